@@ -1,0 +1,232 @@
+/*
+ * rtc.h — C-ABI of the MI355X-native render path for the Ray Tracer Challenge
+ * world model of przemo199/ray-tracer-challenge-rs.
+ *
+ * This is the drop-in boundary.  It replaces, for one
+ * frame, the reference's
+ *     Camera::render           ray-tracer/src/composites/camera.rs:79-95
+ *     Camera::render_parallel  ray-tracer/src/composites/camera.rs:97-112
+ * and, per ray,
+ *     World::color_at          ray-tracer/src/composites/world.rs:89-95
+ * with a HIP wavefront tracer for gfx950.  The reference's only caller of the
+ * render loop is ray-tracer-cli/src/main.rs:18-21; a GPU variant is a third
+ * RenderingMode arm there (ray-tracer-cli/src/cli/rendering_mode.rs:3-7).
+ *
+ * Conventions (mirroring the reference's ownership rules):
+ *   - every input is a plain POD array in f64, i.e. exactly the values the
+ *     reference holds on the host (Matrix<4> is [[f64;4];4] row-major,
+ *     primitives/matrix.rs:8);
+ *   - the caller owns every host buffer; the library owns device buffers
+ *     except the explicit *_device entry points, which write into a
+ *     caller-owned device buffer on a caller-supplied HIP stream;
+ *   - return 0 (RT_OK) on success, a negative rt_status on failure;
+ *     rt_last_error() gives a thread-local message.  The reference panics
+ *     instead (release profile panic=abort, Cargo.toml:16); a host wrapper
+ *     mirroring it turns a negative status into a panic/exception;
+ *   - one context drives one GPU and is used from one host thread at a time;
+ *     launches of one context are issued on one stream in order;
+ *   - there is NO CPU fallback: without a usable HIP device every entry
+ *     point that computes returns RT_ERR_NO_DEVICE.
+ */
+#ifndef RTC_H
+#define RTC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* Image tile rendered by one workgroup; also the row-block unit of shards. */
+#define RT_TILE_W 16
+#define RT_TILE_H 16
+
+/* World::MAX_REFLECTION_ITERATIONS, ray-tracer/src/composites/world.rs:15 */
+#define RT_DEFAULT_MAX_DEPTH 6
+/* largest recursion depth the device ray pool is sized for */
+#define RT_MAX_SUPPORTED_DEPTH 16
+
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID = -1,      /* bad argument / malformed descriptor       */
+    RT_ERR_HIP = -2,          /* a HIP runtime call failed                 */
+    RT_ERR_NO_DEVICE = -3,    /* no HIP device / extension not usable      */
+    RT_ERR_NO_SCENE = -4,     /* render before rt_scene_upload             */
+    RT_ERR_OOM = -5,          /* device allocation failed                  */
+    RT_ERR_POOL = -6,         /* device ray pool overflow (never expected) */
+    RT_ERR_IO = -7            /* file / parse error (scene loader)         */
+} rt_status;
+
+/* Shape kinds: ray-tracer/src/shapes.rs:1-17 */
+typedef enum rt_shape_kind {
+    RT_SHAPE_SPHERE = 0,   /* shapes/sphere.rs   */
+    RT_SHAPE_PLANE = 1,    /* shapes/plane.rs    */
+    RT_SHAPE_CUBE = 2,     /* shapes/cube.rs     */
+    RT_SHAPE_CYLINDER = 3, /* shapes/cylinder.rs */
+    RT_SHAPE_CONE = 4,     /* shapes/cone.rs     */
+    RT_SHAPE_TRIANGLE = 5  /* shapes/triangle.rs */
+} rt_shape_kind;
+
+/* Pattern kinds: ray-tracer/src/patterns.rs:1-14 (+ test-only TestPattern,
+ * patterns/pattern.rs:29-66, which the reference's own world tests use). */
+typedef enum rt_pattern_kind {
+    RT_PATTERN_STRIPE = 0,   /* patterns/stripe_pattern.rs   */
+    RT_PATTERN_GRADIENT = 1, /* patterns/gradient_pattern.rs */
+    RT_PATTERN_RING = 2,     /* patterns/ring_pattern.rs     */
+    RT_PATTERN_CHECKER = 3,  /* patterns/checker_pattern.rs  */
+    RT_PATTERN_COMPLEX = 4,  /* patterns/complex_pattern.rs  */
+    RT_PATTERN_TEST = 5      /* patterns/pattern.rs:29-66    */
+} rt_pattern_kind;
+
+typedef enum rt_precision {
+    RT_PRECISION_F32 = 0, /* the throughput path (north star: f32)          */
+    RT_PRECISION_F64 = 1  /* parity path: same op order / FMA sites as ref  */
+} rt_precision;
+
+typedef enum rt_out_format {
+    RT_OUT_REAL = 0, /* f32 RGB (precision f32) or f64 RGB (precision f64)  */
+    RT_OUT_U8 = 1    /* u8 RGB, round(clamp(c,0,1)*255): canvas.rs:117-123  */
+} rt_out_format;
+
+/* One entry of World.shapes (world.rs:9-12).  The shape's inverse transform
+ * is what Transform::transformation_inverse() returns (shapes/shape.rs:6-14);
+ * the library never inverts, so host and device see the same f64 inverse. */
+typedef struct rt_shape_desc {
+    int32_t kind;        /* rt_shape_kind                                  */
+    int32_t material;    /* index into the material table                  */
+    double inverse[16];  /* row-major Matrix<4>                            */
+    double minimum;      /* cylinder/cone `min` (cylinder.rs:12, cone.rs:12) */
+    double maximum;      /* cylinder/cone `max`                            */
+    int32_t closed;      /* cylinder/cone `closed`                         */
+    int32_t reserved;
+    double vertex_1[3];  /* triangle.rs:12-17 */
+    double edge_1[3];
+    double edge_2[3];
+    double normal[3];
+} rt_shape_desc;
+
+/* composites/material.rs:9-20 */
+typedef struct rt_material_desc {
+    double color[3];
+    double ambient;
+    double diffuse;
+    double specular;
+    double shininess;
+    double reflectiveness;
+    double transparency;
+    double refractive_index;
+    int32_t casts_shadow;
+    int32_t pattern; /* index into the pattern table, -1 = None */
+} rt_material_desc;
+
+/* One Arc<dyn Pattern> (patterns/pattern.rs:6-15). */
+typedef struct rt_pattern_desc {
+    int32_t kind;       /* rt_pattern_kind                                 */
+    int32_t sub_a;      /* ComplexPattern pattern_a (index), else -1       */
+    int32_t sub_b;      /* ComplexPattern pattern_b (index), else -1       */
+    int32_t reserved;
+    double color_a[3];
+    double color_b[3];
+    double inverse[16]; /* pattern transformation_inverse, row-major       */
+} rt_pattern_desc;
+
+/* primitives/light.rs:6-10 */
+typedef struct rt_light_desc {
+    double position[3];
+    double intensity[3];
+} rt_light_desc;
+
+/* The private state of Camera (camera.rs:10-19) after Camera::new
+ * (camera.rs:25-49) and set_transformation (camera.rs:124-127). */
+typedef struct rt_camera_desc {
+    uint32_t width;
+    uint32_t height;
+    double field_of_view;
+    double half_width;
+    double half_height;
+    double pixel_size;
+    double inverse[16]; /* camera transformation_inverse, row-major */
+    double origin[3];   /* inverse * Point::ORIGIN (camera.rs:114-116)  */
+} rt_camera_desc;
+
+typedef struct rt_render_options {
+    uint32_t max_depth;    /* `remaining` of the primary ray; 6 = reference */
+    uint32_t precision;    /* rt_precision                                  */
+    uint32_t out_format;   /* rt_out_format                                 */
+    uint32_t shard_index;  /* row-block sharding            */
+    uint32_t shard_count;  /* 1 = the whole image                           */
+    uint32_t flags;        /* reserved, 0                                   */
+} rt_render_options;
+
+/* Ray counts in the reference's semantics plus the terms of
+ * the algorithmic-FLOP convention. */
+typedef struct rt_stats {
+    uint64_t primary;        /* camera rays (or rays handed to rt_color_at) */
+    uint64_t shadow;         /* L per shaded hit (world.rs:46-52)           */
+    uint64_t reflect;        /* spawned reflection rays (world.rs:114-128)  */
+    uint64_t refract;        /* spawned refraction rays (world.rs:130-157)  */
+    uint64_t shaded;         /* shaded hits (prepare_computations calls)    */
+    uint64_t lit_patterned;  /* light evaluations on a patterned material   */
+    uint64_t refract_evals;  /* refracted_color past the opaque/depth check */
+    uint64_t schlick_evals;  /* schlicks_approximation calls                */
+    double kernel_ms;        /* device time of the render launch            */
+    double algorithmic_flops;/* SURVEY.md §8d convention                    */
+} rt_stats;
+
+typedef struct rt_context rt_context;
+
+int rt_abi_version(void);
+const char* rt_last_error(void);
+int rt_device_count(int* count);
+
+int rt_context_create(int device_ordinal, rt_context** out);
+int rt_context_destroy(rt_context* ctx);
+
+/* Flatten + upload a world.  Replaces the World value that Camera::render
+ * borrows (camera.rs:79).  Tables are copied; the caller may free them. */
+int rt_scene_upload(rt_context* ctx,
+                    const rt_shape_desc* shapes, uint32_t n_shapes,
+                    const rt_material_desc* materials, uint32_t n_materials,
+                    const rt_pattern_desc* patterns, uint32_t n_patterns,
+                    const rt_light_desc* lights, uint32_t n_lights);
+
+/* Rows of the strip one shard writes (RT_TILE_H-row blocks, cyclic). */
+int rt_shard_rows(uint32_t height, uint32_t shard_count, uint32_t* rows);
+
+/* Synchronous render into a caller-owned HOST buffer: Camera::render /
+ * render_parallel semantics (camera.rs:79-112).  Output is row-major, y = 0
+ * on top (canvas.rs:53-55); 3 channels per pixel of f32/f64/u8. With
+ * shard_count > 1 the buffer holds this shard's strip (rt_shard_rows rows). */
+int rt_render(rt_context* ctx, const rt_camera_desc* camera,
+              const rt_render_options* options, void* out_host,
+              rt_stats* stats);
+
+/* Asynchronous render into a caller-owned DEVICE buffer on `hip_stream`
+ * (a hipStream_t, NULL = the context's own stream).  No host sync. */
+int rt_render_device(rt_context* ctx, const rt_camera_desc* camera,
+                     const rt_render_options* options, void* out_device,
+                     void* hip_stream);
+
+/* Batch World::color_at (world.rs:89-95): rays[i] = {ox,oy,oz,dx,dy,dz},
+ * out[i] = RGB, both f64 host arrays; `max_depth` = remaining. */
+int rt_color_at(rt_context* ctx, const double* rays, uint64_t n_rays,
+                uint32_t max_depth, uint32_t precision, double* out_rgb,
+                rt_stats* stats);
+
+/* Cumulative device counters since context creation (after a sync). */
+int rt_read_counters(rt_context* ctx, rt_stats* totals);
+
+/* De-interleave gathered shard strips (shard-major, each rt_shard_rows tall)
+ * into one row-major image on the device, on `hip_stream`. */
+int rt_assemble_shards(rt_context* ctx, const void* gathered_device,
+                       uint32_t width, uint32_t height, uint32_t shard_count,
+                       uint32_t bytes_per_pixel, void* image_device,
+                       void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RTC_H */

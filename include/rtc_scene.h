@@ -1,0 +1,66 @@
+/*
+ * rtc_scene.h — host-side scene input for the render path (C-ABI).
+ *
+ * Mirrors the reference's scene construction API so a caller can go from the
+ * YAML scene files to the descriptor tables rt_scene_upload() takes:
+ *   load_scene_description(path) -> (World, Camera)
+ *       ray-tracer-cli/src/scene_loader.rs:361-367   -> rt_scene_load_yaml
+ *   Camera::new + set_transformation(view_transform(from, to, up))
+ *       scene_loader.rs:255-266, camera.rs:25-49/124-127,
+ *       transformations.rs:75-87                      -> rt_camera_make
+ *   Matrix<4>::inverse  primitives/matrix.rs:247-258  -> rt_matrix_inverse
+ * All arithmetic is f64 and follows the reference's operation order, so the
+ * tables are bit-identical to what the reference holds after loading.
+ * Pure host code: none of these functions needs a GPU.
+ */
+#ifndef RTC_SCENE_H
+#define RTC_SCENE_H
+
+#include "rtc.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rt_scene rt_scene;
+
+typedef struct rt_scene_view {
+    const rt_shape_desc* shapes;
+    uint32_t n_shapes;
+    const rt_material_desc* materials;
+    uint32_t n_materials;
+    const rt_pattern_desc* patterns;
+    uint32_t n_patterns;
+    const rt_light_desc* lights;
+    uint32_t n_lights;
+    rt_camera_desc camera;
+    /* Pairs of value-identical shapes.  The reference identifies shapes by
+     * value in the refraction containers walk (intersection.rs:37-62); the
+     * device identifies them by index.  0 means both agree. */
+    uint32_t duplicate_shapes;
+} rt_scene_view;
+
+/* load_scene_description (scene_loader.rs:361-367).  RT_ERR_IO on a parse
+ * error, with the reason in rt_last_error(). */
+int rt_scene_load_yaml(const char* path, rt_scene** out);
+int rt_scene_load_yaml_text(const char* text, rt_scene** out);
+int rt_scene_view_get(const rt_scene* scene, rt_scene_view* view);
+void rt_scene_free(rt_scene* scene);
+
+/* Camera::new(width, height, fov) + set_transformation(view_transform(...)) */
+int rt_camera_make(uint32_t width, uint32_t height, double field_of_view,
+                   const double from[3], const double to[3], const double up[3],
+                   rt_camera_desc* out);
+
+/* Re-run Camera::new for a new canvas size, keeping fov and transform —
+ * equivalent to editing the YAML camera width/height. */
+int rt_camera_resize(rt_camera_desc* camera, uint32_t width, uint32_t height);
+
+/* Matrix<4>::inverse, row-major 16 doubles. */
+int rt_matrix_inverse(const double m[16], double out[16]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RTC_SCENE_H */

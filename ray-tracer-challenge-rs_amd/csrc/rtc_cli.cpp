@@ -1,0 +1,90 @@
+// rtc_cli.cpp — command-line driver mirroring ray-tracer-cli/src/main.rs:11-31
+// (`<SCENE> <OUT> [-q]`, timing of the render call only, main.rs:17-24) for the
+// GPU render path.  Extra flags: --width/--height (same as editing the YAML
+// camera size), --depth (World::MAX_REFLECTION_ITERATIONS = 6 by default),
+// --precision f32|f64, --device N.  Writes a binary PPM (P6) quantized as
+// canvas.rs:117-123 does.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rtc.h"
+#include "../../include/rtc_scene.h"
+
+static int usage() {
+    std::fprintf(stderr,
+                 "usage: rtc <SCENE.yaml> <OUT.ppm> [-q] [--width W] [--height H] [--depth D]\n"
+                 "           [--precision f32|f64] [--device N]\n");
+    return 2;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 3) return usage();
+    const char* scene_path = argv[1];
+    const char* out_path = argv[2];
+    bool quiet = false;
+    uint32_t width = 0, height = 0, depth = RT_DEFAULT_MAX_DEPTH, precision = RT_PRECISION_F32;
+    int device = 0;
+    for (int i = 3; i < argc; ++i) {
+        std::string a = argv[i];
+        auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : nullptr; };
+        if (a == "-q" || a == "--quiet") quiet = true;
+        else if (a == "--width") { const char* v = next(); if (!v) return usage(); width = (uint32_t)std::atoi(v); }
+        else if (a == "--height") { const char* v = next(); if (!v) return usage(); height = (uint32_t)std::atoi(v); }
+        else if (a == "--depth") { const char* v = next(); if (!v) return usage(); depth = (uint32_t)std::atoi(v); }
+        else if (a == "--device") { const char* v = next(); if (!v) return usage(); device = std::atoi(v); }
+        else if (a == "--precision") {
+            const char* v = next();
+            if (!v) return usage();
+            precision = std::strcmp(v, "f64") == 0 ? RT_PRECISION_F64 : RT_PRECISION_F32;
+        } else return usage();
+    }
+    if (!quiet) std::printf("Rendering scene: %s\n", scene_path);
+    rt_scene* scene = nullptr;
+    if (rt_scene_load_yaml(scene_path, &scene) != RT_OK) {
+        std::fprintf(stderr, "error: %s\n", rt_last_error());
+        return 1;
+    }
+    rt_scene_view v;
+    rt_scene_view_get(scene, &v);
+    rt_camera_desc cam = v.camera;
+    if (width || height) rt_camera_resize(&cam, width ? width : cam.width, height ? height : cam.height);
+    rt_context* ctx = nullptr;
+    if (rt_context_create(device, &ctx) != RT_OK ||
+        rt_scene_upload(ctx, v.shapes, v.n_shapes, v.materials, v.n_materials, v.patterns, v.n_patterns, v.lights,
+                        v.n_lights) != RT_OK) {
+        std::fprintf(stderr, "error: %s\n", rt_last_error());
+        return 1;
+    }
+    rt_render_options o = {depth, precision, RT_OUT_U8, 0, 1, 0};
+    std::vector<uint8_t> img((size_t)cam.width * cam.height * 3);
+    rt_stats st;
+    auto t0 = std::chrono::steady_clock::now();
+    if (rt_render(ctx, &cam, &o, img.data(), &st) != RT_OK) {
+        std::fprintf(stderr, "error: %s\n", rt_last_error());
+        return 1;
+    }
+    double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!quiet) {
+        std::printf("Image rendered in: %.3fs (kernel %.3f ms)\n", s, st.kernel_ms);
+        const double rays = (double)(st.primary + st.shadow + st.reflect + st.refract);
+        std::printf("rays: primary %llu shadow %llu reflect %llu refract %llu (%.1f Mray/s kernel)\n",
+                    (unsigned long long)st.primary, (unsigned long long)st.shadow, (unsigned long long)st.reflect,
+                    (unsigned long long)st.refract, rays / (st.kernel_ms * 1e3));
+    }
+    FILE* f = std::fopen(out_path, "wb");
+    if (!f) {
+        std::fprintf(stderr, "error: cannot write %s\n", out_path);
+        return 1;
+    }
+    std::fprintf(f, "P6\n%u %u\n255\n", cam.width, cam.height);
+    std::fwrite(img.data(), 1, img.size(), f);
+    std::fclose(f);
+    if (!quiet) std::printf("Image saved to: %s\n", out_path);
+    rt_context_destroy(ctx);
+    rt_scene_free(scene);
+    return 0;
+}

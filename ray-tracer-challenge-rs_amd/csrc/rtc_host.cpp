@@ -1,0 +1,554 @@
+// rtc_host.cpp — the C-ABI of include/rtc.h: context, world flattening and
+// upload, launch of the gfx950 kernels, counters.
+//
+// Boundary it replaces: Camera::render / render_parallel
+// (camera.rs:79-112) borrow `&World` and return an owned Canvas; here the
+// caller hands the World as POD tables once (rt_scene_upload) and gets the
+// canvas written into its own buffer per frame (rt_render / rt_render_device).
+// There is no CPU fallback: without a HIP device every call that computes
+// fails with RT_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/rtc.h"
+#include "flop_model.hpp"
+#include "rtc_internal.hpp"
+
+namespace rtc {
+
+template <typename R>
+hipError_t launch_trace(const LaunchParams<R>& P, bool pool, uint32_t grid, size_t dyn_lds, hipStream_t stream);
+template <typename R>
+hipError_t occupancy(bool pool, size_t dyn_lds, int* blocks_per_cu);
+hipError_t launch_assemble(const void* gathered, void* image, uint32_t width, uint32_t height, uint32_t shards,
+                           uint32_t strip_rows, uint32_t bpp, hipStream_t stream);
+
+namespace {
+thread_local std::string g_error;
+}
+
+int set_error(int code, const std::string& msg) {
+    g_error = msg;
+    return code;
+}
+
+#define RT_HIP(call)                                                                               \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return set_error(RT_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));       \
+    } while (0)
+
+// World tables cast to R and laid out per kind (rtc_internal.hpp).
+template <typename R>
+struct DeviceWorld {
+    ShapeRec<R>* shapes = nullptr;
+    MaterialRec<R>* materials = nullptr;
+    PatternRec<R>* patterns = nullptr;
+    LightRec<R>* lights = nullptr;
+    DevScene<R> scene{};
+    void release() {
+        (void)hipFree(shapes);
+        (void)hipFree(materials);
+        (void)hipFree(patterns);
+        (void)hipFree(lights);
+        shapes = nullptr;
+        materials = nullptr;
+        patterns = nullptr;
+        lights = nullptr;
+    }
+};
+
+}  // namespace rtc
+
+struct rt_context {
+    int device = 0;
+    int cu_count = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    unsigned long long* d_tile_counter = nullptr;
+    unsigned long long tile_base = 0;
+    unsigned long long* d_counters = nullptr;  // kNumCounters cumulative
+    int32_t* d_error = nullptr;
+    bool have_scene = false;
+    rtc::DeviceWorld<float> w32;
+    rtc::DeviceWorld<double> w64;
+    rtc::FlopScene flops;  // per-kind shape counts for the algorithmic FLOP model
+    void* d_scratch = nullptr;  // host-buffer renders / color_at staging
+    size_t scratch_bytes = 0;
+};
+
+namespace rtc {
+namespace {
+
+template <typename T>
+int upload(T** dst, const std::vector<T>& v) {
+    if (v.empty()) {
+        *dst = nullptr;
+        return RT_OK;
+    }
+    RT_HIP(hipMalloc(reinterpret_cast<void**>(dst), v.size() * sizeof(T)));
+    RT_HIP(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+template <typename R>
+int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes, uint32_t ns,
+                const rt_material_desc* mats, uint32_t nm, const rt_pattern_desc* pats, uint32_t np,
+                const rt_light_desc* lights, uint32_t nl) {
+    (void)ctx;
+    w.release();
+    std::vector<ShapeRec<R>> sh;
+    std::vector<int32_t> begin(kNumKinds + 1, 0);
+    for (int k = 0; k < kNumKinds; ++k) {
+        begin[k] = (int32_t)sh.size();
+        for (uint32_t i = 0; i < ns; ++i) {
+            const rt_shape_desc& d = shapes[i];
+            if (d.kind != k) continue;
+            ShapeRec<R> r{};
+            for (int q = 0; q < 12; ++q) r.inv[q] = (R)d.inverse[q];
+            r.ymin = (R)d.minimum;
+            r.ymax = (R)d.maximum;
+            for (int q = 0; q < 3; ++q) {
+                r.tri[q] = (R)d.vertex_1[q];
+                r.tri[3 + q] = (R)d.edge_1[q];
+                r.tri[6 + q] = (R)d.edge_2[q];
+                r.tri[9 + q] = (R)d.normal[q];
+            }
+            r.world_index = (int32_t)i;
+            r.material = d.material;
+            r.closed = d.closed ? 1 : 0;
+            r.casts_shadow = mats[d.material].casts_shadow ? 1 : 0;
+            sh.push_back(r);
+        }
+    }
+    begin[kNumKinds] = (int32_t)sh.size();
+    std::vector<MaterialRec<R>> mt(nm);
+    bool any_secondary = false;
+    for (uint32_t i = 0; i < nm; ++i) {
+        const rt_material_desc& d = mats[i];
+        MaterialRec<R>& m = mt[i];
+        for (int q = 0; q < 3; ++q) m.color[q] = (R)d.color[q];
+        m.ambient = (R)d.ambient;
+        m.diffuse = (R)d.diffuse;
+        m.specular = (R)d.specular;
+        m.shininess = (R)d.shininess;
+        m.reflectiveness = (R)d.reflectiveness;
+        m.transparency = (R)d.transparency;
+        m.refractive_index = (R)d.refractive_index;
+        m.pattern = d.pattern;
+        m.casts_shadow = d.casts_shadow;
+        if (d.reflectiveness != 0.0 || d.transparency != 0.0) any_secondary = true;
+    }
+    std::vector<PatternRec<R>> pt(np);
+    for (uint32_t i = 0; i < np; ++i) {
+        const rt_pattern_desc& d = pats[i];
+        PatternRec<R>& p = pt[i];
+        for (int q = 0; q < 3; ++q) {
+            p.color_a[q] = (R)d.color_a[q];
+            p.color_b[q] = (R)d.color_b[q];
+        }
+        for (int q = 0; q < 12; ++q) p.inv[q] = (R)d.inverse[q];
+        p.kind = d.kind;
+        p.sub_a = d.sub_a;
+        p.sub_b = d.sub_b;
+    }
+    std::vector<LightRec<R>> lt(nl);
+    for (uint32_t i = 0; i < nl; ++i)
+        for (int q = 0; q < 3; ++q) {
+            lt[i].position[q] = (R)lights[i].position[q];
+            lt[i].intensity[q] = (R)lights[i].intensity[q];
+        }
+    int rc;
+    if ((rc = upload(&w.shapes, sh)) || (rc = upload(&w.materials, mt)) || (rc = upload(&w.patterns, pt)) ||
+        (rc = upload(&w.lights, lt)))
+        return rc;
+    w.scene.shapes = w.shapes;
+    w.scene.materials = w.materials;
+    w.scene.patterns = w.patterns;
+    w.scene.lights = w.lights;
+    for (int k = 0; k <= kNumKinds; ++k) w.scene.kind_begin[k] = begin[k];
+    w.scene.n_lights = (int32_t)nl;
+    w.scene.any_secondary = any_secondary ? 1 : 0;
+    return RT_OK;
+}
+
+int validate_scene(const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats, uint32_t nm,
+                   const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights, uint32_t nl) {
+    if ((ns && !shapes) || (nm && !mats) || (np && !pats) || (nl && !lights))
+        return set_error(RT_ERR_INVALID, "rt_scene_upload: null table with nonzero count");
+    for (uint32_t i = 0; i < ns; ++i) {
+        if (shapes[i].kind < 0 || shapes[i].kind >= kNumKinds)
+            return set_error(RT_ERR_INVALID, "shape " + std::to_string(i) + ": unknown kind");
+        if (shapes[i].material < 0 || (uint32_t)shapes[i].material >= nm)
+            return set_error(RT_ERR_INVALID, "shape " + std::to_string(i) + ": material index out of range");
+    }
+    for (uint32_t i = 0; i < nm; ++i)
+        if (mats[i].pattern >= 0 && (uint32_t)mats[i].pattern >= np)
+            return set_error(RT_ERR_INVALID, "material " + std::to_string(i) + ": pattern index out of range");
+    for (uint32_t i = 0; i < np; ++i) {
+        if (pats[i].kind < 0 || pats[i].kind > RT_PATTERN_TEST)
+            return set_error(RT_ERR_INVALID, "pattern " + std::to_string(i) + ": unknown kind");
+        if (pats[i].kind == RT_PATTERN_COMPLEX &&
+            (pats[i].sub_a < 0 || pats[i].sub_b < 0 || (uint32_t)pats[i].sub_a >= np || (uint32_t)pats[i].sub_b >= np))
+            return set_error(RT_ERR_INVALID, "pattern " + std::to_string(i) + ": bad sub-pattern index");
+    }
+    if (ns > 0x7fffffff || nl > 0x7fffffff) return set_error(RT_ERR_INVALID, "table too large");
+    return RT_OK;
+}
+
+uint32_t tile_rows_for(uint32_t height, uint32_t shards, uint32_t shard) {
+    const uint32_t trows = (height + RT_TILE_H - 1) / RT_TILE_H;
+    return trows > shard ? (trows - shard + shards - 1) / shards : 0;
+}
+
+// Rays held by the LDS pool for a given depth and pop batch (LIFO bound).
+uint32_t pool_capacity(uint32_t depth, uint32_t batch) { return (uint32_t)kBlock + depth * batch; }
+
+template <typename R>
+size_t pool_lds_bytes(uint32_t cap) {
+    return 3 * kBlock * sizeof(long long) + (size_t)cap * (7 * sizeof(R) + sizeof(uint32_t));
+}
+
+constexpr size_t kMaxLds = 160 * 1024 - 1024;  // leave room for static LDS
+
+struct LaunchShape {
+    bool pool;
+    uint32_t grid;
+    size_t lds;
+    uint32_t cap, batch;
+};
+
+template <typename R>
+int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t n_tiles, LaunchShape& ls) {
+    ls.pool = sc.any_secondary && depth > 0;
+    ls.lds = 0;
+    ls.cap = ls.batch = 0;
+    if (ls.pool) {
+        uint32_t batch = kBlock;
+        while (batch > 32 && pool_lds_bytes<R>(pool_capacity(depth, batch)) > kMaxLds) batch /= 2;
+        if (pool_lds_bytes<R>(pool_capacity(depth, batch)) > kMaxLds)
+            return set_error(RT_ERR_INVALID, "max_depth too large for the LDS ray pool");
+        ls.batch = batch;
+        ls.cap = pool_capacity(depth, batch);
+        ls.lds = pool_lds_bytes<R>(ls.cap);
+    }
+    int per_cu = 0;
+    RT_HIP(occupancy<R>(ls.pool, ls.lds, &per_cu));
+    if (per_cu < 1) per_cu = 1;
+    const uint64_t resident = (uint64_t)per_cu * (uint64_t)ctx->cu_count;
+    ls.grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, resident));
+    return RT_OK;
+}
+
+template <typename R>
+int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const double* d_rays, uint64_t n_rays,
+           uint32_t depth, uint32_t out_format, uint32_t shard_index, uint32_t shard_count, void* out_device,
+           hipStream_t stream) {
+    LaunchParams<R> P{};
+    P.scene = w.scene;
+    if (cam) {
+        for (int q = 0; q < 12; ++q) P.cam.inv[q] = (R)cam->inverse[q];
+        for (int q = 0; q < 3; ++q) P.cam.origin[q] = (R)cam->origin[q];
+        P.cam.half_width = (R)cam->half_width;
+        P.cam.half_height = (R)cam->half_height;
+        P.cam.pixel_size = (R)cam->pixel_size;
+        P.width = cam->width;
+        P.height = cam->height;
+        P.tiles_x = (cam->width + RT_TILE_W - 1) / RT_TILE_W;
+        P.tile_rows = tile_rows_for(cam->height, shard_count, shard_index);
+        P.n_tiles = P.tiles_x * P.tile_rows;
+    } else {
+        P.rays = d_rays;
+        P.n_rays = n_rays;
+        P.n_tiles = (uint32_t)((n_rays + kBlock - 1) / kBlock);
+    }
+    P.out = out_device;
+    P.out_format = out_format;
+    P.shard_index = shard_index;
+    P.shard_count = shard_count;
+    P.max_depth = depth;
+    P.tile_counter = ctx->d_tile_counter;
+    P.counters = ctx->d_counters;
+    P.error_flag = ctx->d_error;
+    if (P.n_tiles == 0) return RT_OK;
+    LaunchShape ls;
+    int rc = plan_launch<R>(ctx, w.scene, depth, P.n_tiles, ls);
+    if (rc) return rc;
+    P.pool_capacity = ls.cap;
+    P.pop_batch = ls.batch;
+    P.tile_base = ctx->tile_base;
+    // every launched workgroup makes exactly one failing dequeue at the end
+    ctx->tile_base += (unsigned long long)P.n_tiles + ls.grid;
+    RT_HIP(launch_trace<R>(P, ls.pool, ls.grid, ls.lds, stream));
+    return RT_OK;
+}
+
+int check_ready(rt_context* ctx) {
+    if (!ctx) return set_error(RT_ERR_INVALID, "null context");
+    if (!ctx->have_scene) return set_error(RT_ERR_NO_SCENE, "render before rt_scene_upload");
+    return RT_OK;
+}
+
+int check_options(const rt_render_options* o) {
+    if (!o) return set_error(RT_ERR_INVALID, "null options");
+    if (o->precision > RT_PRECISION_F64) return set_error(RT_ERR_INVALID, "unknown precision");
+    if (o->out_format > RT_OUT_U8) return set_error(RT_ERR_INVALID, "unknown output format");
+    if (o->max_depth > RT_MAX_SUPPORTED_DEPTH) return set_error(RT_ERR_INVALID, "max_depth above RT_MAX_SUPPORTED_DEPTH");
+    if (o->shard_count == 0 || o->shard_index >= o->shard_count) return set_error(RT_ERR_INVALID, "bad shard");
+    return RT_OK;
+}
+
+int ensure_scratch(rt_context* ctx, size_t bytes) {
+    if (ctx->scratch_bytes >= bytes) return RT_OK;
+    if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    ctx->d_scratch = nullptr;
+    ctx->scratch_bytes = 0;
+    RT_HIP(hipMalloc(&ctx->d_scratch, bytes));
+    ctx->scratch_bytes = bytes;
+    return RT_OK;
+}
+
+int read_counters(rt_context* ctx, unsigned long long out[kNumCounters]) {
+    RT_HIP(hipMemcpy(out, ctx->d_counters, kNumCounters * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+void fill_stats(rt_context* ctx, const unsigned long long before[kNumCounters],
+                const unsigned long long after[kNumCounters], float ms, rt_stats* s) {
+    uint64_t d[kNumCounters];
+    for (int i = 0; i < kNumCounters; ++i) d[i] = after[i] - before[i];
+    s->primary = d[0];
+    s->shadow = d[1];
+    s->reflect = d[2];
+    s->refract = d[3];
+    s->shaded = d[4];
+    s->lit_patterned = d[5];
+    s->refract_evals = d[6];
+    s->schlick_evals = d[7];
+    s->kernel_ms = ms;
+    s->algorithmic_flops = algorithmic_flops(ctx->flops, *s);
+}
+
+int check_pool_error(rt_context* ctx) {
+    int32_t err = 0;
+    RT_HIP(hipMemcpy(&err, ctx->d_error, sizeof(err), hipMemcpyDeviceToHost));
+    if (err) {
+        RT_HIP(hipMemset(ctx->d_error, 0, sizeof(int32_t)));
+        return set_error(RT_ERR_POOL, "device ray pool overflow");
+    }
+    return RT_OK;
+}
+
+}  // namespace
+}  // namespace rtc
+
+using namespace rtc;
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+const char* rt_last_error(void) { return rtc::g_error.c_str(); }
+
+int rt_device_count(int* count) {
+    if (!count) return set_error(RT_ERR_INVALID, "null count");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return RT_OK;
+}
+
+int rt_context_create(int device_ordinal, rt_context** out) {
+    if (!out) return set_error(RT_ERR_INVALID, "null out");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return set_error(RT_ERR_NO_DEVICE, "no HIP device available (the render path has no CPU fallback)");
+    if (device_ordinal < 0 || device_ordinal >= n) return set_error(RT_ERR_INVALID, "device ordinal out of range");
+    auto ctx = std::make_unique<rt_context>();
+    ctx->device = device_ordinal;
+    RT_HIP(hipSetDevice(device_ordinal));
+    hipDeviceProp_t prop;
+    RT_HIP(hipGetDeviceProperties(&prop, device_ordinal));
+    ctx->cu_count = prop.multiProcessorCount;
+    RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    RT_HIP(hipEventCreate(&ctx->ev_start));
+    RT_HIP(hipEventCreate(&ctx->ev_stop));
+    RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_tile_counter), sizeof(unsigned long long)));
+    RT_HIP(hipMemset(ctx->d_tile_counter, 0, sizeof(unsigned long long)));
+    RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_counters), kNumCounters * sizeof(unsigned long long)));
+    RT_HIP(hipMemset(ctx->d_counters, 0, kNumCounters * sizeof(unsigned long long)));
+    RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_error), sizeof(int32_t)));
+    RT_HIP(hipMemset(ctx->d_error, 0, sizeof(int32_t)));
+    *out = ctx.release();
+    return RT_OK;
+}
+
+int rt_context_destroy(rt_context* ctx) {
+    if (!ctx) return RT_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    ctx->w32.release();
+    ctx->w64.release();
+    (void)hipFree(ctx->d_tile_counter);
+    (void)hipFree(ctx->d_counters);
+    (void)hipFree(ctx->d_error);
+    (void)hipFree(ctx->d_scratch);
+    if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
+    if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return RT_OK;
+}
+
+int rt_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats,
+                    uint32_t nm, const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights,
+                    uint32_t nl) {
+    if (!ctx) return set_error(RT_ERR_INVALID, "null context");
+    int rc = validate_scene(shapes, ns, mats, nm, pats, np, lights, nl);
+    if (rc) return rc;
+    RT_HIP(hipSetDevice(ctx->device));
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->have_scene = false;
+    if ((rc = build_world<float>(ctx, ctx->w32, shapes, ns, mats, nm, pats, np, lights, nl))) return rc;
+    if ((rc = build_world<double>(ctx, ctx->w64, shapes, ns, mats, nm, pats, np, lights, nl))) return rc;
+    ctx->flops = FlopScene{};
+    for (uint32_t i = 0; i < ns; ++i) {
+        const rt_shape_desc& d = shapes[i];
+        ctx->flops.per_ray += shape_test_flops(d.kind, d.closed != 0);
+    }
+    ctx->flops.n_lights = nl;
+    ctx->have_scene = true;
+    return RT_OK;
+}
+
+int rt_shard_rows(uint32_t height, uint32_t shard_count, uint32_t* rows) {
+    if (!rows || shard_count == 0) return set_error(RT_ERR_INVALID, "bad arguments");
+    *rows = tile_rows_for(height, shard_count, 0) * RT_TILE_H;
+    return RT_OK;
+}
+
+int rt_render_device(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, void* out_device,
+                     void* hip_stream) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if ((rc = check_options(o))) return rc;
+    if (!cam || !out_device) return set_error(RT_ERR_INVALID, "null camera or output");
+    if (cam->width == 0 || cam->height == 0) return RT_OK;  // empty canvas (canvas.rs:27-35)
+    RT_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    if (o->precision == RT_PRECISION_F32)
+        return launch<float>(ctx, ctx->w32, cam, nullptr, 0, o->max_depth, o->out_format, o->shard_index,
+                             o->shard_count, out_device, s);
+    return launch<double>(ctx, ctx->w64, cam, nullptr, 0, o->max_depth, o->out_format, o->shard_index,
+                          o->shard_count, out_device, s);
+}
+
+int rt_render(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, void* out_host,
+              rt_stats* stats) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if ((rc = check_options(o))) return rc;
+    if (!cam || !out_host) return set_error(RT_ERR_INVALID, "null camera or output");
+    RT_HIP(hipSetDevice(ctx->device));
+    const size_t elem = o->out_format == RT_OUT_U8 ? 1 : (o->precision == RT_PRECISION_F32 ? 4 : 8);
+    const uint32_t rows = tile_rows_for(cam->height, o->shard_count, o->shard_index) * RT_TILE_H;
+    const uint32_t valid_rows = o->shard_count == 1 ? cam->height : rows;
+    const size_t bytes = (size_t)rows * cam->width * 3 * elem;
+    if (bytes == 0) {
+        if (stats) std::memset(stats, 0, sizeof(*stats));
+        return RT_OK;
+    }
+    if ((rc = ensure_scratch(ctx, bytes))) return rc;
+    RT_HIP(hipMemsetAsync(ctx->d_scratch, 0, bytes, ctx->stream));
+    unsigned long long before[kNumCounters], after[kNumCounters];
+    if ((rc = read_counters(ctx, before))) return rc;
+    RT_HIP(hipEventRecord(ctx->ev_start, ctx->stream));
+    if ((rc = rt_render_device(ctx, cam, o, ctx->d_scratch, ctx->stream))) return rc;
+    RT_HIP(hipEventRecord(ctx->ev_stop, ctx->stream));
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    float ms = 0.f;
+    RT_HIP(hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_stop));
+    RT_HIP(hipMemcpy(out_host, ctx->d_scratch, (size_t)valid_rows * cam->width * 3 * elem, hipMemcpyDeviceToHost));
+    if ((rc = check_pool_error(ctx))) return rc;
+    if (stats) {
+        if ((rc = read_counters(ctx, after))) return rc;
+        fill_stats(ctx, before, after, ms, stats);
+    }
+    return RT_OK;
+}
+
+int rt_color_at(rt_context* ctx, const double* rays, uint64_t n, uint32_t depth, uint32_t precision, double* out,
+                rt_stats* stats) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (!rays || !out) return set_error(RT_ERR_INVALID, "null rays or output");
+    if (precision > RT_PRECISION_F64) return set_error(RT_ERR_INVALID, "unknown precision");
+    if (depth > RT_MAX_SUPPORTED_DEPTH) return set_error(RT_ERR_INVALID, "max_depth above RT_MAX_SUPPORTED_DEPTH");
+    if (n == 0) {
+        if (stats) std::memset(stats, 0, sizeof(*stats));
+        return RT_OK;
+    }
+    RT_HIP(hipSetDevice(ctx->device));
+    const size_t elem = precision == RT_PRECISION_F32 ? 4 : 8;
+    const size_t in_bytes = n * 6 * sizeof(double), out_bytes = n * 3 * elem;
+    if ((rc = ensure_scratch(ctx, in_bytes + out_bytes))) return rc;
+    double* d_rays = static_cast<double*>(ctx->d_scratch);
+    void* d_out = static_cast<char*>(ctx->d_scratch) + in_bytes;
+    RT_HIP(hipMemcpy(d_rays, rays, in_bytes, hipMemcpyHostToDevice));
+    unsigned long long before[kNumCounters], after[kNumCounters];
+    if ((rc = read_counters(ctx, before))) return rc;
+    RT_HIP(hipEventRecord(ctx->ev_start, ctx->stream));
+    if (precision == RT_PRECISION_F32)
+        rc = launch<float>(ctx, ctx->w32, nullptr, d_rays, n, depth, RT_OUT_REAL, 0, 1, d_out, ctx->stream);
+    else
+        rc = launch<double>(ctx, ctx->w64, nullptr, d_rays, n, depth, RT_OUT_REAL, 0, 1, d_out, ctx->stream);
+    if (rc) return rc;
+    RT_HIP(hipEventRecord(ctx->ev_stop, ctx->stream));
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    float ms = 0.f;
+    RT_HIP(hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_stop));
+    if (precision == RT_PRECISION_F32) {
+        std::vector<float> tmp(n * 3);
+        RT_HIP(hipMemcpy(tmp.data(), d_out, out_bytes, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < n * 3; ++i) out[i] = tmp[i];
+    } else {
+        RT_HIP(hipMemcpy(out, d_out, out_bytes, hipMemcpyDeviceToHost));
+    }
+    if ((rc = check_pool_error(ctx))) return rc;
+    if (stats) {
+        if ((rc = read_counters(ctx, after))) return rc;
+        fill_stats(ctx, before, after, ms, stats);
+    }
+    return RT_OK;
+}
+
+int rt_read_counters(rt_context* ctx, rt_stats* totals) {
+    if (!ctx || !totals) return set_error(RT_ERR_INVALID, "null argument");
+    RT_HIP(hipSetDevice(ctx->device));
+    RT_HIP(hipDeviceSynchronize());
+    unsigned long long zero[kNumCounters] = {}, now[kNumCounters];
+    int rc = read_counters(ctx, now);
+    if (rc) return rc;
+    fill_stats(ctx, zero, now, 0.f, totals);
+    return check_pool_error(ctx);
+}
+
+int rt_assemble_shards(rt_context* ctx, const void* gathered, uint32_t width, uint32_t height, uint32_t shards,
+                       uint32_t bpp, void* image, void* hip_stream) {
+    if (!ctx || !gathered || !image || shards == 0 || bpp == 0) return set_error(RT_ERR_INVALID, "bad arguments");
+    RT_HIP(hipSetDevice(ctx->device));
+    uint32_t rows = 0;
+    rt_shard_rows(height, shards, &rows);
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    RT_HIP(launch_assemble(gathered, image, width, height, shards, rows, bpp, s));
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,115 @@
+// rtc_internal.hpp — records shared by the host launcher (rtc_host.cpp) and
+// the gfx950 kernels (rtc_kernels.hip).
+//
+// HBM layout of a flattened world (SURVEY.md §7 "SoA per-type shape tables"):
+// the reference's Vec<Box<dyn Shape>> (world.rs:11) becomes ONE array of
+// fixed-size ShapeRec sorted by kind (spheres, planes, cubes, cylinders,
+// cones, triangles), with `kind_begin[k]..kind_begin[k+1]` delimiting the
+// per-type loops.  Every lane of a wave walks the same records in the same
+// order, so the shape loads are wave-uniform scalar (s_load) loads that hit
+// the scalar cache; `world_index` restores the reference's world order for
+// the stable-sort tie rule.  Materials, patterns and
+// lights are small side tables.  Everything is cast once from the caller's
+// f64 tables to the kernel's real type R (f32 or f64).
+#pragma once
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/rtc.h"
+
+namespace rtc {
+
+int set_error(int code, const std::string& msg);  // rtc_host.cpp (thread-local)
+
+constexpr int kBlock = 256;        // threads per workgroup = 4 waves of 64
+constexpr int kTilePixels = RT_TILE_W * RT_TILE_H;  // one tile per workgroup pass
+static_assert(kTilePixels == kBlock, "one pixel per thread per tile");
+constexpr int kNumKinds = 6;
+constexpr int kNumCounters = 8;    // order of rt_stats' first eight fields
+
+// Fixed-point pixel accumulator of the pool kernel: contributions are summed
+// as int64 multiples of 2^-48 so the per-pixel sum is independent of the
+// (nondeterministic) order in which waves add to it.
+constexpr double kAccScale = 281474976710656.0;  // 2^48
+constexpr double kAccInvScale = 1.0 / 281474976710656.0;
+
+template <typename R>
+struct alignas(16) ShapeRec {
+    R inv[12];     // rows 0..2 of transformation_inverse (row 3 is never read:
+                   // Mul<Point>/Mul<Vector> produce 3 rows, matrix.rs:332-362)
+    R ymin, ymax;  // cylinder/cone min/max (cylinder.rs:12-14)
+    R tri[12];     // triangle vertex_1, edge_1, edge_2, normal (triangle.rs:12-17)
+    int32_t world_index;
+    int32_t material;
+    int32_t closed;
+    int32_t casts_shadow;  // material.casts_shadow, hoisted for the any-hit loop
+};
+
+template <typename R>
+struct alignas(16) MaterialRec {
+    R color[3];
+    R ambient, diffuse, specular, shininess;
+    R reflectiveness, transparency, refractive_index;
+    int32_t pattern;       // -1 = None
+    int32_t casts_shadow;
+};
+
+template <typename R>
+struct alignas(16) PatternRec {
+    R color_a[3];
+    R color_b[3];
+    R inv[12];
+    int32_t kind;
+    int32_t sub_a, sub_b;
+    int32_t pad;
+};
+
+template <typename R>
+struct alignas(16) LightRec {
+    R position[3];
+    R intensity[3];
+};
+
+template <typename R>
+struct CameraRec {
+    R inv[12];
+    R origin[3];
+    R half_width, half_height, pixel_size;
+};
+
+template <typename R>
+struct DevScene {
+    const ShapeRec<R>* shapes;
+    const MaterialRec<R>* materials;
+    const PatternRec<R>* patterns;
+    const LightRec<R>* lights;
+    int32_t kind_begin[kNumKinds + 1];
+    int32_t n_lights;
+    int32_t any_secondary;  // some material has reflectiveness or transparency != 0
+};
+
+// One launch of the tracer.
+template <typename R>
+struct LaunchParams {
+    DevScene<R> scene;
+    CameraRec<R> cam;
+    const double* rays;      // color_at mode: n_rays x {o, d} (f64), else null
+    uint64_t n_rays;
+    void* out;               // row-major RGB of R (RT_OUT_REAL) or u8 (RT_OUT_U8)
+    uint32_t out_format;
+    uint32_t width, height;  // canvas
+    uint32_t tiles_x;        // tiles per row
+    uint32_t tile_rows;      // tile rows of THIS shard's strip
+    uint32_t shard_index, shard_count;
+    uint32_t n_tiles;        // tiles_x * tile_rows (or ray chunks in color_at mode)
+    uint32_t max_depth;      // `remaining` of the primary ray
+    uint32_t pool_capacity;  // pool kernel: rays held in LDS
+    uint32_t pop_batch;      // pool kernel: rays popped per iteration (<= kBlock)
+    unsigned long long* tile_counter;  // cumulative dequeue counter
+    unsigned long long tile_base;      // its value at this launch's start
+    unsigned long long* counters;      // kNumCounters cumulative u64
+    int32_t* error_flag;               // set nonzero on pool overflow
+};
+
+}  // namespace rtc

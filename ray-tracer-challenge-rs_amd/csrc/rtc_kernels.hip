@@ -1,0 +1,925 @@
+// rtc_kernels.hip — the MI355X (gfx950, wave64) render path.
+//
+// Replaces Camera::render[_parallel] (camera.rs:79-112) and the
+// World::color_at -> collect_intersections -> shade_hit recursion
+// (world.rs:25-157) with two persistent-threads kernels:
+//
+//  * trace_direct  — one thread per pixel, no ray pool.  Used when no ray can
+//    spawn a child (no material with reflectiveness/transparency != 0, or
+//    max_depth == 0): the whole per-pixel tree is one shaded hit plus L shadow
+//    rays.  This is three_sphere_scene, the BASELINE metric's config.
+//  * trace_pool    — wavefront tracer.  A workgroup owns a 16x16 tile; the
+//    tile's rays live in LDS (SoA) as a LIFO pool.  Each iteration pops up to
+//    `pop_batch` rays, traces them one per lane (closest hit, shading, any-hit
+//    shadow rays), accumulates weight x surface colour into the tile's pixel
+//    accumulators, and pushes the reflection/refraction children, compacted
+//    per wave with ballot + mbcnt and ONE LDS atomic per wave.  LIFO popping
+//    bounds the pool at tile + depth x pop_batch rays (host sizes it).
+//    The recursion is linear in scalar weights (world.rs:54-66, 127, 156), so
+//    pixel = sum over tree nodes of (product of weights) x surface colour.
+//
+// Tiles are handed out by a cumulative atomic counter (dynamic load balance
+// over a grid sized to the resident workgroup count).  World tables are read
+// with wave-uniform scalar loads in per-type loops (rtc_internal.hpp).
+//
+// Two instantiations: R = float (the throughput path) and R = double (parity:
+// the reference's operation order, its FMA sites and EPSILON = 8e-8; the TU
+// is compiled with -ffp-contract=off so nothing else is fused).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <climits>
+#include <cstdint>
+
+#include "rtc_internal.hpp"
+
+namespace rtc {
+
+// ------------------------------------------------------------ real traits
+template <typename R>
+struct Real;
+
+template <>
+struct Real<float> {
+    static constexpr float kEps = 8e-8f;        // guards (consts.rs:2)
+    static constexpr float kOffset = 1e-4f;     // over/under point + cap normals:
+                                                // 8e-8 is below the f32 ulp at |p|>0.7
+    static constexpr float kMax = FLT_MAX;      // consts.rs:8 analogue
+    static constexpr float kInf = __builtin_huge_valf();
+    // reference `a * b + c` (unfused there): fused here for throughput
+    __device__ static inline float madd(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+    // reference `mul_add` sites
+    __device__ static inline float rfma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+    __device__ static inline float div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+    __device__ static inline float sqrt(float a) { return __builtin_amdgcn_sqrtf(a); }
+    __device__ static inline float rsqrt(float a) { return __builtin_amdgcn_rsqf(a); }
+    __device__ static inline float pow(float x, float y) {  // x in (0, 1] here
+        return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+    }
+    __device__ static inline float floor(float a) { return __builtin_floorf(a); }
+    __device__ static inline float trunc(float a) { return __builtin_truncf(a); }
+    __device__ static inline float fabs(float a) { return __builtin_fabsf(a); }
+    __device__ static inline float fmax(float a, float b) { return __builtin_fmaxf(a, b); }
+    __device__ static inline float fmin(float a, float b) { return __builtin_fminf(a, b); }
+};
+
+template <>
+struct Real<double> {
+    static constexpr double kEps = 0.00000008;
+    static constexpr double kOffset = 0.00000008;  // computed_hit.rs:33-34
+    static constexpr double kMax = DBL_MAX;
+    static constexpr double kInf = __builtin_huge_val();
+    __device__ static inline double madd(double a, double b, double c) { return a * b + c; }
+    __device__ static inline double rfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+    __device__ static inline double div(double a, double b) { return a / b; }
+    __device__ static inline double sqrt(double a) { return __builtin_sqrt(a); }
+    __device__ static inline double rsqrt(double a) { return 1.0 / __builtin_sqrt(a); }
+    __device__ static inline double pow(double x, double y) { return ::pow(x, y); }
+    __device__ static inline double floor(double a) { return __builtin_floor(a); }
+    __device__ static inline double trunc(double a) { return __builtin_trunc(a); }
+    __device__ static inline double fabs(double a) { return __builtin_fabs(a); }
+    __device__ static inline double fmax(double a, double b) { return __builtin_fmax(a, b); }
+    __device__ static inline double fmin(double a, double b) { return __builtin_fmin(a, b); }
+};
+
+template <typename R>
+struct V3 {
+    R x, y, z;
+};
+
+template <typename R>
+__device__ inline V3<R> v3(R x, R y, R z) {
+    return {x, y, z};
+}
+template <typename R>
+__device__ inline V3<R> vsub(V3<R> a, V3<R> b) {
+    return {a.x - b.x, a.y - b.y, a.z - b.z};
+}
+template <typename R>
+__device__ inline V3<R> vneg(V3<R> a) {
+    return {-a.x, -a.y, -a.z};
+}
+// vector.rs:93-95
+template <typename R>
+__device__ inline R dot(V3<R> a, V3<R> b) {
+    return Real<R>::rfma(a.z, b.z, Real<R>::rfma(a.x, b.x, a.y * b.y));
+}
+// vector.rs:97-103
+template <typename R>
+__device__ inline V3<R> cross(V3<R> a, V3<R> b) {
+    return {Real<R>::rfma(a.y, b.z, -a.z * b.y), Real<R>::rfma(a.z, b.x, -a.x * b.z),
+            Real<R>::rfma(a.x, b.y, -a.y * b.x)};
+}
+// vector.rs:84-91
+template <typename R>
+__device__ inline V3<R> normalized(V3<R> v) {
+    if constexpr (sizeof(R) == 4) {
+        const R inv = Real<R>::rsqrt(Real<R>::madd(v.z, v.z, Real<R>::madd(v.y, v.y, v.x * v.x)));
+        return {v.x * inv, v.y * inv, v.z * inv};
+    } else {
+        const R m = Real<R>::sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+        return {v.x / m, v.y / m, v.z / m};
+    }
+}
+template <typename R>
+__device__ inline R magnitude(V3<R> v) {
+    if constexpr (sizeof(R) == 4)
+        return Real<R>::sqrt(Real<R>::madd(v.z, v.z, Real<R>::madd(v.y, v.y, v.x * v.x)));
+    else
+        return Real<R>::sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+}
+// vector.rs:105-107: v - (n * 2) * v.dot(n)
+template <typename R>
+__device__ inline V3<R> reflect(V3<R> v, V3<R> n) {
+    const R d = dot(v, n);
+    return {v.x - (n.x * R(2)) * d, v.y - (n.y * R(2)) * d, v.z - (n.z * R(2)) * d};
+}
+// ray.rs:30-32 / computed_hit.rs:33-34: p + d * t
+template <typename R>
+__device__ inline V3<R> along(V3<R> p, V3<R> d, R t) {
+    return {Real<R>::madd(d.x, t, p.x), Real<R>::madd(d.y, t, p.y), Real<R>::madd(d.z, t, p.z)};
+}
+
+// matrix.rs:332-346 (w = 1), left fold from 0.0
+template <typename R>
+__device__ inline V3<R> xform_point(const R* m, V3<R> p) {
+    if constexpr (sizeof(R) == 4) {
+        return {__builtin_fmaf(m[2], p.z, __builtin_fmaf(m[1], p.y, __builtin_fmaf(m[0], p.x, m[3]))),
+                __builtin_fmaf(m[6], p.z, __builtin_fmaf(m[5], p.y, __builtin_fmaf(m[4], p.x, m[7]))),
+                __builtin_fmaf(m[10], p.z, __builtin_fmaf(m[9], p.y, __builtin_fmaf(m[8], p.x, m[11])))};
+    } else {
+        return {((((R)0 + m[0] * p.x) + m[1] * p.y) + m[2] * p.z) + m[3],
+                ((((R)0 + m[4] * p.x) + m[5] * p.y) + m[6] * p.z) + m[7],
+                ((((R)0 + m[8] * p.x) + m[9] * p.y) + m[10] * p.z) + m[11]};
+    }
+}
+// matrix.rs:348-362 (w = 0)
+template <typename R>
+__device__ inline V3<R> xform_vector(const R* m, V3<R> v) {
+    if constexpr (sizeof(R) == 4) {
+        return {__builtin_fmaf(m[2], v.z, __builtin_fmaf(m[1], v.y, m[0] * v.x)),
+                __builtin_fmaf(m[6], v.z, __builtin_fmaf(m[5], v.y, m[4] * v.x)),
+                __builtin_fmaf(m[10], v.z, __builtin_fmaf(m[9], v.y, m[8] * v.x))};
+    } else {
+        return {(((R)0 + m[0] * v.x) + m[1] * v.y) + m[2] * v.z + m[3] * (R)0,
+                (((R)0 + m[4] * v.x) + m[5] * v.y) + m[6] * v.z + m[7] * (R)0,
+                (((R)0 + m[8] * v.x) + m[9] * v.y) + m[10] * v.z + m[11] * (R)0};
+    }
+}
+// transpose(inverse) * n (shape.rs:25), 3x3 part
+template <typename R>
+__device__ inline V3<R> xform_normal(const R* m, V3<R> n) {
+    if constexpr (sizeof(R) == 4) {
+        return {__builtin_fmaf(m[8], n.z, __builtin_fmaf(m[4], n.y, m[0] * n.x)),
+                __builtin_fmaf(m[9], n.z, __builtin_fmaf(m[5], n.y, m[1] * n.x)),
+                __builtin_fmaf(m[10], n.z, __builtin_fmaf(m[6], n.y, m[2] * n.x))};
+    } else {
+        return {(((R)0 + m[0] * n.x) + m[4] * n.y) + m[8] * n.z,
+                (((R)0 + m[1] * n.x) + m[5] * n.y) + m[9] * n.z,
+                (((R)0 + m[2] * n.x) + m[6] * n.y) + m[10] * n.z};
+    }
+}
+
+// f64/f32 `as i64` (saturating, NaN -> 0); only the parity bit is used
+template <typename R>
+__device__ inline bool odd_i64(R v) {
+    if (!(v == v)) return false;                     // NaN -> 0
+    const R lim = (R)9.2233720368547758e18;          // 2^63
+    if (v >= lim) return true;                       // saturates to i64::MAX (odd)
+    if (v <= -lim) return false;                     // saturates to i64::MIN (even)
+    const long long i = (long long)v;
+    return (i & 1) != 0;
+}
+
+// -------------------------------------------------------- shape intersect
+// Each routine calls emit(t) once per entry, in the reference's push order.
+
+// utils.rs:47-57
+template <typename R, typename F>
+__device__ inline void quadratic(R a, R b, R c, F&& emit2) {
+    const R disc = Real<R>::rfma((R)4 * a, -c, b * b);
+    if (disc < (R)0) return;
+    const R da = (R)2 * a;
+    const R root = Real<R>::sqrt(disc);
+    if constexpr (sizeof(R) == 4) {
+        const R ri = __builtin_amdgcn_rcpf(da);
+        emit2((-b - root) * ri, (-b + root) * ri);
+    } else {
+        emit2((-b - root) / da, (-b + root) / da);
+    }
+}
+
+template <typename R, int K, typename F>
+__device__ inline void entries(const ShapeRec<R>& s, V3<R> o, V3<R> d, F&& emit) {
+    using T = Real<R>;
+    if constexpr (K == RT_SHAPE_SPHERE) {  // sphere.rs:41-53
+        const R a = dot(d, d);
+        const R b = (R)2 * dot(d, o);
+        const R c = dot(o, o) - (R)1;
+        quadratic<R>(a, b, c, [&](R t1, R t2) {
+            emit(t1);
+            emit(t2);
+        });
+    } else if constexpr (K == RT_SHAPE_PLANE) {  // plane.rs:42-48
+        if (T::fabs(d.y) < T::kEps) return;
+        emit(T::div(-o.y, d.y));
+    } else if constexpr (K == RT_SHAPE_CUBE) {  // cube.rs:22-43, 65-85
+        auto axis = [&](R org, R dir, R& lo, R& hi) {
+            const R nmin = (R)-1 - org, nmax = (R)1 - org;
+            if (T::fabs(dir) >= T::kEps) {
+                if constexpr (sizeof(R) == 4) {
+                    const R r = __builtin_amdgcn_rcpf(dir);
+                    lo = nmin * r;
+                    hi = nmax * r;
+                } else {
+                    lo = nmin / dir;
+                    hi = nmax / dir;
+                }
+            } else {
+                lo = nmin * T::kMax;
+                hi = nmax * T::kMax;
+            }
+            if (lo > hi) {
+                const R tmp = lo;
+                lo = hi;
+                hi = tmp;
+            }
+        };
+        R xn, xx, yn, yx, zn, zx;
+        axis(o.x, d.x, xn, xx);
+        axis(o.y, d.y, yn, yx);
+        axis(o.z, d.z, zn, zx);
+        const R tmin = T::fmax(T::fmax(T::fmax(-T::kMax, xn), yn), zn);
+        const R tmax = T::fmin(T::fmin(T::fmin(T::kMax, xx), yx), zx);
+        if (tmin < tmax && tmax > (R)0) {
+            emit(tmin);
+            emit(tmax);
+        }
+    } else if constexpr (K == RT_SHAPE_CYLINDER || K == RT_SHAPE_CONE) {
+        const R ymin = s.ymin, ymax = s.ymax;
+        auto side = [&](R t1, R t2) {
+            if (t1 > t2) {
+                const R tmp = t1;
+                t1 = t2;
+                t2 = tmp;
+            }
+            R y1, y2;
+            if constexpr (K == RT_SHAPE_CYLINDER) {  // cylinder.rs:96-104
+                y1 = T::rfma(t1, d.y, o.y);
+                y2 = T::rfma(t2, d.y, o.y);
+            } else {  // cone.rs:99-107
+                y1 = T::rfma(d.y, t1, o.y);
+                y2 = T::rfma(d.y, t2, o.y);
+            }
+            if (ymin < y1 && y1 < ymax) emit(t1);
+            if (ymin < y2 && y2 < ymax) emit(t2);
+        };
+        if constexpr (K == RT_SHAPE_CYLINDER) {  // cylinder.rs:81-110
+            const R a = d.x * d.x + d.z * d.z;
+            if (T::fabs(a) > (R)0) {
+                const R b = (R)2 * T::rfma(o.x, d.x, o.z * d.z);
+                const R c = o.x * o.x + o.z * o.z - (R)1;
+                quadratic<R>(a, b, c, side);
+            }
+        } else {  // cone.rs:81-112
+            const R a = d.x * d.x - d.y * d.y + d.z * d.z;
+            const R b = (R)2 * T::rfma(o.z, d.z, T::rfma(o.x, d.x, -o.y * d.y));
+            const R c = o.x * o.x - o.y * o.y + o.z * o.z;
+            if (T::fabs(a) < T::kEps && T::fabs(b) > T::kEps)
+                emit(T::div(-c, (R)2 * b));
+            else
+                quadratic<R>(a, b, c, side);
+        }
+        // intersect_caps: cylinder.rs:41-58 / cone.rs:41-58
+        if (!s.closed || T::fabs(d.y) < T::kEps) return;
+        const R r_lo = (K == RT_SHAPE_CYLINDER) ? (R)1 : ymin * ymin;
+        const R r_hi = (K == RT_SHAPE_CYLINDER) ? (R)1 : ymax * ymax;
+        R t = T::div(ymin - o.y, d.y);
+        R x = T::rfma(d.x, t, o.x), z = T::rfma(d.z, t, o.z);
+        if (x * x + z * z <= r_lo) emit(t);
+        t = T::div(ymax - o.y, d.y);
+        x = T::rfma(d.x, t, o.x);
+        z = T::rfma(d.z, t, o.z);
+        if (x * x + z * z <= r_hi) emit(t);
+    } else {  // triangle.rs:39-56
+        const V3<R> e1 = {s.tri[3], s.tri[4], s.tri[5]};
+        const V3<R> e2 = {s.tri[6], s.tri[7], s.tri[8]};
+        const V3<R> dce2 = cross(d, e2);
+        const R det = dot(e1, dce2);
+        if (T::fabs(det) < T::kEps) return;
+        const V3<R> v1o = vsub(o, V3<R>{s.tri[0], s.tri[1], s.tri[2]});
+        const R u = T::div(dot(v1o, dce2), det);
+        if (!(u >= (R)0 && u <= (R)1)) return;
+        const V3<R> oce1 = cross(v1o, e1);
+        const R v = T::div(dot(d, oce1), det);
+        if (v > (R)0 && u + v < (R)1) emit(T::div(dot(e2, oce1), det));
+    }
+}
+
+// Visit every shape of kind K (wave-uniform loop, scalar loads).
+template <typename R, int K, typename F>
+__device__ inline void for_kind(const DevScene<R>& sc, F&& f) {
+    const int b = sc.kind_begin[K], e = sc.kind_begin[K + 1];
+    for (int i = b; i < e; ++i) f(sc.shapes[i], i);
+}
+
+template <typename R, typename F>
+__device__ inline void for_all_kinds(const DevScene<R>& sc, F&& f) {
+    for_kind<R, RT_SHAPE_SPHERE>(sc, [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_SPHERE>(s, i); });
+    for_kind<R, RT_SHAPE_PLANE>(sc, [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_PLANE>(s, i); });
+    for_kind<R, RT_SHAPE_CUBE>(sc, [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_CUBE>(s, i); });
+    for_kind<R, RT_SHAPE_CYLINDER>(sc,
+                                   [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_CYLINDER>(s, i); });
+    for_kind<R, RT_SHAPE_CONE>(sc, [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_CONE>(s, i); });
+    for_kind<R, RT_SHAPE_TRIANGLE>(sc,
+                                   [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_TRIANGLE>(s, i); });
+}
+
+template <typename R>
+struct Hit {
+    R t;
+    int slot;   // index into the kind-sorted shape table, -1 = miss
+    int world;  // world order, for the stable-sort tie rule
+    int entry;  // push order within the shape
+    int kind;
+};
+
+// collect_intersections + hit (world.rs:25-35, intersections.rs:13-18):
+// the first minimum t >= 0 in (t, world order, push order).
+template <typename R>
+__device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
+    Hit<R> h{Real<R>::kInf, -1, INT_MAX, 0, -1};
+    for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
+        const V3<R> lo = xform_point(s.inv, o);
+        const V3<R> ld = xform_vector(s.inv, d);
+        const int w = s.world_index;
+        int e = 0;
+        entries<R, K>(s, lo, ld, [&](R t) {
+            if (t >= (R)0 && (t < h.t || (t == h.t && w < h.world))) {
+                h.t = t;
+                h.slot = slot;
+                h.world = w;
+                h.entry = e;
+                h.kind = K;
+            }
+            ++e;
+        });
+    });
+    return h;
+}
+
+// is_in_shadow (world.rs:98-112): any casting shape with 0 <= t < distance.
+template <typename R>
+__device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) {
+    bool hit = false;
+    for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int) {
+        if (!s.casts_shadow) return;
+        const V3<R> lo = xform_point(s.inv, o);
+        const V3<R> ld = xform_vector(s.inv, d);
+        entries<R, K>(s, lo, ld, [&](R t) { hit = hit || (t >= (R)0 && t < dist); });
+    });
+    return hit;
+}
+
+// Refractive-index containers walk (intersection.rs:33-62) without a list:
+// a shape is inside the container list iff an odd number of its entries sort
+// before the hit; the list's `last()` is the present shape whose last entry
+// before the hit sorts latest.  Keys sort by (t, world order, push order).
+template <typename R>
+__device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> d, const Hit<R>& h, R& n1,
+                                          R& n2) {
+    struct Key {
+        R t;
+        int w, e;
+    };
+    auto before = [](const Key& a, const Key& b) {
+        return a.t < b.t || (a.t == b.t && (a.w < b.w || (a.w == b.w && a.e < b.e)));
+    };
+    const Key hk{h.t, h.world, h.entry};
+    bool have_all = false, have_other = false, hit_present = false;
+    Key best_all{}, best_other{};
+    int mat_all = -1, mat_other = -1;
+    for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
+        const V3<R> lo = xform_point(s.inv, o);
+        const V3<R> ld = xform_vector(s.inv, d);
+        const int w = s.world_index;
+        int e = 0, count = 0;
+        Key last{};
+        entries<R, K>(s, lo, ld, [&](R t) {
+            const Key k{t, w, e};
+            if (before(k, hk)) {
+                ++count;
+                if (count == 1 || before(last, k)) last = k;
+            }
+            ++e;
+        });
+        if (count & 1) {
+            if (!have_all || before(best_all, last)) {
+                best_all = last;
+                mat_all = s.material;
+                have_all = true;
+            }
+            if (slot == h.slot) {
+                hit_present = true;
+            } else if (!have_other || before(best_other, last)) {
+                best_other = last;
+                mat_other = s.material;
+                have_other = true;
+            }
+        }
+    });
+    n1 = have_all ? sc.materials[mat_all].refractive_index : (R)1;
+    if (hit_present)  // the hit removes itself from the list
+        n2 = have_other ? sc.materials[mat_other].refractive_index : (R)1;
+    else              // the hit pushes itself
+        n2 = sc.materials[sc.shapes[h.slot].material].refractive_index;
+}
+
+// shape.rs:22-27 + local_normal_at of each shape
+template <typename R>
+__device__ inline V3<R> normal_at(const ShapeRec<R>& s, int kind, V3<R> p) {
+    using T = Real<R>;
+    const V3<R> lp = xform_point(s.inv, p);
+    V3<R> ln;
+    switch (kind) {
+        case RT_SHAPE_SPHERE: ln = lp; break;                          // sphere.rs:57-59
+        case RT_SHAPE_PLANE: ln = {(R)0, (R)1, (R)0}; break;          // plane.rs:52-54
+        case RT_SHAPE_CUBE: {                                          // cube.rs:89-101
+            const R ax = T::fabs(lp.x), ay = T::fabs(lp.y), az = T::fabs(lp.z);
+            const R mx = T::fmax(T::fmax(T::fmax(-T::kMax, ax), ay), az);
+            auto near = [](R a, R b) { return a == b || T::fabs(a - b) < T::kEps; };
+            if (near(mx, ax)) ln = {lp.x, (R)0, (R)0};
+            else if (near(mx, ay)) ln = {(R)0, lp.y, (R)0};
+            else ln = {(R)0, (R)0, lp.z};
+            break;
+        }
+        case RT_SHAPE_CYLINDER: {  // cylinder.rs:114-126
+            const R dist = lp.x * lp.x + lp.z * lp.z;
+            if (dist < (R)1 && lp.y >= s.ymax - T::kOffset) ln = {(R)0, (R)1, (R)0};
+            else if (dist < (R)1 && lp.y <= s.ymin + T::kOffset) ln = {(R)0, (R)-1, (R)0};
+            else ln = {lp.x, (R)0, lp.z};
+            break;
+        }
+        case RT_SHAPE_CONE: {  // cone.rs:116-133
+            const R dist = lp.x * lp.x + lp.z * lp.z;
+            if (dist < s.ymax * s.ymax && lp.y >= s.ymax - T::kOffset) ln = {(R)0, (R)1, (R)0};
+            else if (dist < s.ymin * s.ymin && lp.y <= s.ymin + T::kOffset) ln = {(R)0, (R)-1, (R)0};
+            else {
+                R y = T::sqrt(dist);
+                if (lp.y > (R)0) y = -y;
+                ln = {lp.x, y, lp.z};
+            }
+            break;
+        }
+        default: ln = {s.tri[9], s.tri[10], s.tri[11]}; break;  // triangle.rs:78-80
+    }
+    return normalized(xform_normal(s.inv, ln));
+}
+
+// Pattern::color_at_shape (pattern.rs:10-14) and the five color_at bodies.
+template <typename R>
+__device__ inline V3<R> pattern_color(const DevScene<R>& sc, int pid, const ShapeRec<R>& s, V3<R> p) {
+    using T = Real<R>;
+    const PatternRec<R>* pr = &sc.patterns[pid];
+    const V3<R> pp = xform_point(pr->inv, xform_point(s.inv, p));
+    for (int guard = 0; guard < 16; ++guard) {
+        switch (pr->kind) {
+            case RT_PATTERN_STRIPE:  // stripe_pattern.rs:24-31
+                return odd_i64(T::floor(pp.x)) ? v3(pr->color_b[0], pr->color_b[1], pr->color_b[2])
+                                                : v3(pr->color_a[0], pr->color_a[1], pr->color_a[2]);
+            case RT_PATTERN_GRADIENT: {  // gradient_pattern.rs:24-31 (ping-pong)
+                R f = T::fabs(pp.x - T::trunc(pp.x));
+                if (odd_i64(pp.x)) f = (R)1 - f;
+                return {pr->color_a[0] + (pr->color_b[0] - pr->color_a[0]) * f,
+                        pr->color_a[1] + (pr->color_b[1] - pr->color_a[1]) * f,
+                        pr->color_a[2] + (pr->color_b[2] - pr->color_a[2]) * f};
+            }
+            case RT_PATTERN_RING: {  // ring_pattern.rs:25-32
+                const R r = T::floor(T::sqrt(pp.x * pp.x + pp.z * pp.z));
+                return odd_i64(r) ? v3(pr->color_b[0], pr->color_b[1], pr->color_b[2])
+                                  : v3(pr->color_a[0], pr->color_a[1], pr->color_a[2]);
+            }
+            case RT_PATTERN_CHECKER: {  // checker_pattern.rs:24-31
+                const R sum = T::floor(pp.x) + T::floor(pp.y) + T::floor(pp.z);
+                return odd_i64(sum) ? v3(pr->color_b[0], pr->color_b[1], pr->color_b[2])
+                                    : v3(pr->color_a[0], pr->color_a[1], pr->color_a[2]);
+            }
+            case RT_PATTERN_COMPLEX:  // complex_pattern.rs:25-32: sub transforms ignored
+                pr = &sc.patterns[odd_i64(T::floor(pp.x)) ? pr->sub_b : pr->sub_a];
+                continue;
+            default:  // TestPattern (pattern.rs:55-58)
+                return pp;
+        }
+    }
+    return {(R)0, (R)0, (R)0};
+}
+
+// Per-thread event counters (rt_stats order).
+struct Counts {
+    uint32_t c[kNumCounters];
+};
+
+// One radiance ray: closest hit, shading over all lights with shadow rays,
+// and the (at most two) children.  Returns false on a miss.
+template <typename R>
+struct Shaded {
+    V3<R> surface;  // Σ_lights lighting(...)  (world.rs:44-52)
+    bool refl_child, refr_child;
+    V3<R> refl_o, refl_d, refr_o, refr_d;
+    R refl_w, refr_w;  // reflectiveness × {R | 1}, transparency × {1-R | 1}
+};
+
+template <typename R, bool kChildren>
+__device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32_t remaining, Shaded<R>& out,
+                                 Counts& k) {
+    using T = Real<R>;
+    const Hit<R> h = closest_hit(sc, o, d);
+    if (h.slot < 0) return false;  // world.rs:85: miss -> BLACK
+    k.c[4]++;                      // shaded
+    const ShapeRec<R>& s = sc.shapes[h.slot];
+    // prepare_computations, intersection.rs:21-31
+    const V3<R> p = along(o, d, h.t);
+    V3<R> n = normal_at(s, h.kind, p);
+    const V3<R> eye = vneg(d);
+    if (dot(n, eye) < (R)0) n = vneg(n);
+    const MaterialRec<R>& m = sc.materials[s.material];
+    const V3<R> over = along(p, n, T::kOffset);  // computed_hit.rs:33
+    // material.rs:75-80: the pattern is sampled at over_point, once per hit
+    V3<R> base = {m.color[0], m.color[1], m.color[2]};
+    const bool patterned = m.pattern >= 0;
+    if (patterned) base = pattern_color(sc, m.pattern, s, over);
+    V3<R> surface = {(R)0, (R)0, (R)0};
+    for (int li = 0; li < sc.n_lights; ++li) {
+        const LightRec<R>& L = sc.lights[li];
+        const V3<R> lpos = {L.position[0], L.position[1], L.position[2]};
+        const V3<R> to_light = vsub(lpos, over);
+        const R dist = magnitude(to_light);
+        const V3<R> ld = normalized(to_light);  // == to_light / dist (world.rs:104-106)
+        const bool shadowed = any_hit(sc, over, ld, dist);
+        k.c[1]++;
+        if (patterned) k.c[5]++;
+        // calculate_lighting, material.rs:83-114
+        const V3<R> eff = {base.x * L.intensity[0], base.y * L.intensity[1], base.z * L.intensity[2]};
+        V3<R> c = {eff.x * m.ambient, eff.y * m.ambient, eff.z * m.ambient};
+        if (!shadowed) {
+            const R ldn = dot(ld, n);
+            if (!(ldn < (R)0)) {
+                c = {c.x + (eff.x * m.diffuse) * ldn, c.y + (eff.y * m.diffuse) * ldn,
+                     c.z + (eff.z * m.diffuse) * ldn};
+                const R rde = dot(reflect(vneg(ld), n), eye);
+                if (!(rde <= (R)0)) {
+                    const R f = T::pow(rde, m.shininess);
+                    c = {c.x + (L.intensity[0] * m.specular) * f, c.y + (L.intensity[1] * m.specular) * f,
+                         c.z + (L.intensity[2] * m.specular) * f};
+                }
+            }
+        }
+        surface = {surface.x + c.x, surface.y + c.y, surface.z + c.z};
+    }
+    out.surface = surface;
+    out.refl_child = out.refr_child = false;
+    if constexpr (kChildren) {
+        const bool reflective = m.reflectiveness > (R)0, transparent = m.transparency > (R)0;
+        R n1 = (R)1, n2 = (R)1;
+        if (m.transparency != (R)0) refractive_indices(sc, o, d, h, n1, n2);
+        // Schlick mixing only when both (world.rs:59-66)
+        R fr = (R)1, ft = (R)1;
+        if (reflective && transparent) {  // computed_hit.rs:50-68
+            k.c[7]++;
+            R cs = dot(eye, n);
+            bool total = false;
+            if (n1 > n2) {
+                const R ratio = T::div(n1, n2);
+                const R sin2 = (ratio * ratio) * ((R)1 - cs * cs);
+                if (sin2 > (R)1) total = true;
+                else cs = T::sqrt((R)1 - sin2);
+            }
+            R rr = (R)1;
+            if (!total) {
+                const R q = T::div(n1 - n2, n1 + n2);
+                const R r0 = q * q;
+                const R x = (R)1 - cs;
+                rr = T::rfma((R)1 - r0, x * ((x * x) * (x * x)), r0);
+            }
+            fr = rr;
+            ft = (R)1 - rr;
+        }
+        if (remaining > 0 && m.reflectiveness != (R)0) {  // world.rs:114-128
+            out.refl_child = true;
+            out.refl_o = over;
+            out.refl_d = reflect(d, n);
+            out.refl_w = m.reflectiveness * fr;
+            k.c[2]++;
+        }
+        if (remaining > 0 && m.transparency != (R)0) {  // world.rs:130-157
+            k.c[6]++;
+            const R nr = T::div(n1, n2);
+            const R cos_i = dot(eye, n);
+            const R sin2_t = (nr * nr) * ((R)1 - cos_i * cos_i);
+            if (!(sin2_t > (R)1)) {
+                const R cos_t = T::sqrt((R)1 - sin2_t);
+                const R f = T::rfma(nr, cos_i, -cos_t);
+                out.refr_child = true;
+                out.refr_o = along(p, n, -T::kOffset);  // under_point, computed_hit.rs:34
+                out.refr_d = {n.x * f - eye.x * nr, n.y * f - eye.y * nr, n.z * f - eye.z * nr};
+                out.refr_w = m.transparency * ft;
+                k.c[3]++;
+            }
+        }
+    }
+    return true;
+}
+
+// camera.rs:52-68
+template <typename R>
+__device__ inline void camera_ray(const CameraRec<R>& c, uint32_t x, uint32_t y, V3<R>& o, V3<R>& d) {
+    const R ox = ((R)x + (R)0.5) * c.pixel_size;
+    const R oy = ((R)y + (R)0.5) * c.pixel_size;
+    const R wx = c.half_width - ox;
+    const R wy = c.half_height - oy;
+    o = {c.origin[0], c.origin[1], c.origin[2]};
+    if constexpr (sizeof(R) == 4) {
+        // pixel - origin == M3 * (wx, wy, -1): skip the cancelling translation
+        d = normalized(xform_vector(c.inv, V3<R>{wx, wy, (R)-1}));
+    } else {
+        const V3<R> pixel = xform_point(c.inv, V3<R>{wx, wy, (R)-1});
+        d = normalized(vsub(pixel, o));
+    }
+}
+
+template <typename R>
+__device__ inline void store_pixel(const LaunchParams<R>& P, uint64_t idx, V3<R> c) {
+    if (P.out_format == RT_OUT_U8) {
+        // canvas.rs:117-123: round(clamp(c, 0, 1) * 255), NaN -> 0
+        auto q = [](R v) -> uint8_t {
+            if (!(v == v)) return 0;
+            v = v < (R)0 ? (R)0 : (v > (R)1 ? (R)1 : v);
+            if constexpr (sizeof(R) == 4) return (uint8_t)__builtin_roundf(v * (R)255);
+            else return (uint8_t)__builtin_round(v * (R)255);
+        };
+        uint8_t* o = static_cast<uint8_t*>(P.out) + 3 * idx;
+        o[0] = q(c.x);
+        o[1] = q(c.y);
+        o[2] = q(c.z);
+    } else {
+        R* o = static_cast<R*>(P.out) + 3 * idx;
+        o[0] = c.x;
+        o[1] = c.y;
+        o[2] = c.z;
+    }
+}
+
+// Tile t of this launch -> pixel of thread `tid` (x, y, output index).
+template <typename R>
+__device__ inline bool tile_pixel(const LaunchParams<R>& P, uint32_t t, uint32_t tid, uint32_t& x, uint32_t& y,
+                                  uint64_t& out_idx) {
+    const uint32_t lrow = t / P.tiles_x, tcol = t - lrow * P.tiles_x;
+    const uint32_t grow = lrow * P.shard_count + P.shard_index;
+    x = tcol * RT_TILE_W + (tid % RT_TILE_W);
+    y = grow * RT_TILE_H + (tid / RT_TILE_W);
+    const uint32_t local_y = lrow * RT_TILE_H + (tid / RT_TILE_W);
+    out_idx = (uint64_t)local_y * P.width + x;
+    return x < P.width && y < P.height;
+}
+
+template <typename R>
+__device__ inline void load_primary(const LaunchParams<R>& P, uint32_t t, uint32_t tid, bool& valid, V3<R>& o,
+                                    V3<R>& d, uint64_t& out_idx) {
+    if (P.rays) {  // color_at mode: tile = 256 consecutive rays
+        const uint64_t r = (uint64_t)t * kBlock + tid;
+        valid = r < P.n_rays;
+        out_idx = r;
+        if (valid) {
+            const double* q = P.rays + 6 * r;
+            o = {(R)q[0], (R)q[1], (R)q[2]};
+            d = {(R)q[3], (R)q[4], (R)q[5]};
+        }
+    } else {
+        uint32_t x, y;
+        valid = tile_pixel(P, t, tid, x, y, out_idx);
+        if (valid) camera_ray(P.cam, x, y, o, d);
+    }
+}
+
+__device__ inline void flush_counts(const Counts& k, unsigned long long* global) {
+    __shared__ unsigned long long s_counts[kNumCounters];
+    if (threadIdx.x < kNumCounters) s_counts[threadIdx.x] = 0;
+    __syncthreads();
+    for (int i = 0; i < kNumCounters; ++i) {
+        // wave reduction, then one LDS atomic per wave
+        unsigned long long v = k.c[i];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&s_counts[i], v);
+    }
+    __syncthreads();
+    if (threadIdx.x < kNumCounters && s_counts[threadIdx.x]) atomicAdd(&global[threadIdx.x], s_counts[threadIdx.x]);
+}
+
+// --------------------------------------------------------------- kernels
+template <typename R>
+__global__ __launch_bounds__(kBlock) void trace_direct(LaunchParams<R> P) {
+    __shared__ unsigned int s_tile[2];
+    Counts k = {};
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t it = 0;; ++it) {
+        if (tid == 0) s_tile[it & 1] = (unsigned int)(atomicAdd(P.tile_counter, 1ull) - P.tile_base);
+        __syncthreads();
+        const uint32_t t = s_tile[it & 1];
+        if (t >= P.n_tiles) break;
+        bool valid;
+        V3<R> o, d;
+        uint64_t out_idx;
+        load_primary(P, t, tid, valid, o, d, out_idx);
+        if (!valid) continue;
+        k.c[0]++;
+        Shaded<R> sh;
+        V3<R> c = {(R)0, (R)0, (R)0};
+        if (shade_ray<R, false>(P.scene, o, d, 0, sh, k)) c = sh.surface;
+        store_pixel(P, out_idx, c);
+    }
+    flush_counts(k, P.counters);
+}
+
+// Ray pool layout in dynamic LDS: [acc: 3 x kBlock i64][ox oy oz dx dy dz w : cap x R][meta : cap x u32]
+template <typename R>
+struct Pool {
+    long long* acc;
+    R *ox, *oy, *oz, *dx, *dy, *dz, *w;
+    uint32_t* meta;  // pixel (bits 0-7) | remaining << 8
+};
+
+// Reserve `pred` slots for the lanes of one wave: ballot + mbcnt prefix, one
+// LDS atomic per wave.  Returns the lane's slot or -1.
+__device__ inline int wave_reserve(bool pred, int* top) {
+    const unsigned long long m = __ballot(pred);
+    if (m == 0) return -1;
+    const int prefix = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(top, __popcll(m));
+    base = __shfl(base, leader);
+    return pred ? base + prefix : -1;
+}
+
+template <typename R>
+__device__ inline void pool_put(const Pool<R>& pl, int slot, V3<R> o, V3<R> d, R w, uint32_t meta) {
+    pl.ox[slot] = o.x;
+    pl.oy[slot] = o.y;
+    pl.oz[slot] = o.z;
+    pl.dx[slot] = d.x;
+    pl.dy[slot] = d.y;
+    pl.dz[slot] = d.z;
+    pl.w[slot] = w;
+    pl.meta[slot] = meta;
+}
+
+__device__ inline void acc_add(long long* acc, uint32_t pix, double v) {
+    const long long q = __double2ll_rn(v * kAccScale);
+    if (q) atomicAdd(reinterpret_cast<unsigned long long*>(&acc[pix]), (unsigned long long)q);
+}
+
+template <typename R>
+__global__ __launch_bounds__(kBlock) void trace_pool(LaunchParams<R> P) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ unsigned int s_tile[2];
+    __shared__ int s_top[2];
+    const uint32_t cap = P.pool_capacity;
+    Pool<R> pl;
+    pl.acc = reinterpret_cast<long long*>(smem);
+    R* base = reinterpret_cast<R*>(smem + 3 * kBlock * sizeof(long long));
+    pl.ox = base;
+    pl.oy = base + cap;
+    pl.oz = base + 2 * cap;
+    pl.dx = base + 3 * cap;
+    pl.dy = base + 4 * cap;
+    pl.dz = base + 5 * cap;
+    pl.w = base + 6 * cap;
+    pl.meta = reinterpret_cast<uint32_t*>(base + 7 * cap);
+
+    Counts k = {};
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t it = 0;; ++it) {
+        if (tid == 0) {
+            s_tile[it & 1] = (unsigned int)(atomicAdd(P.tile_counter, 1ull) - P.tile_base);
+            s_top[0] = 0;
+        }
+        for (int c = 0; c < 3; ++c) pl.acc[c * kBlock + tid] = 0;
+        __syncthreads();
+        const uint32_t t = s_tile[it & 1];
+        if (t >= P.n_tiles) break;
+        bool valid;
+        V3<R> o, d;
+        uint64_t out_idx;
+        load_primary(P, t, tid, valid, o, d, out_idx);
+        if (valid) k.c[0]++;
+        {
+            const int slot = wave_reserve(valid, &s_top[0]);
+            if (valid) pool_put(pl, slot, o, d, (R)1, tid | (P.max_depth << 8));
+        }
+        __syncthreads();
+        for (uint32_t gen = 0;; ++gen) {
+            const int cur = gen & 1;
+            const int size = s_top[cur];
+            if (size == 0) break;
+            const int kpop = size < (int)P.pop_batch ? size : (int)P.pop_batch;
+            const int bottom = size - kpop;
+            const bool active = (int)tid < kpop;
+            V3<R> ro, rd;
+            R rw = (R)0;
+            uint32_t meta = 0;
+            if (active) {
+                const int sl = bottom + (int)tid;
+                ro = {pl.ox[sl], pl.oy[sl], pl.oz[sl]};
+                rd = {pl.dx[sl], pl.dy[sl], pl.dz[sl]};
+                rw = pl.w[sl];
+                meta = pl.meta[sl];
+            }
+            if (tid == 0) s_top[cur ^ 1] = bottom;
+            __syncthreads();  // every lane holds its ray; the next top is set
+            Shaded<R> sh;
+            bool hit = false;
+            if (active) hit = shade_ray<R, true>(P.scene, ro, rd, meta >> 8, sh, k);
+            const uint32_t pix = meta & 0xFFu;
+            if (hit) {
+                acc_add(pl.acc, pix, (double)(sh.surface.x * rw));
+                acc_add(pl.acc + kBlock, pix, (double)(sh.surface.y * rw));
+                acc_add(pl.acc + 2 * kBlock, pix, (double)(sh.surface.z * rw));
+            }
+            const uint32_t child_meta = pix | (((meta >> 8) - 1u) << 8);
+            const bool c1 = hit && sh.refl_child, c2 = hit && sh.refr_child;
+            const int s1 = wave_reserve(c1, &s_top[cur ^ 1]);
+            const int s2 = wave_reserve(c2, &s_top[cur ^ 1]);
+            if (c1) {
+                if (s1 < (int)cap) pool_put(pl, s1, sh.refl_o, sh.refl_d, rw * sh.refl_w, child_meta);
+                else atomicOr(P.error_flag, 1);
+            }
+            if (c2) {
+                if (s2 < (int)cap) pool_put(pl, s2, sh.refr_o, sh.refr_d, rw * sh.refr_w, child_meta);
+                else atomicOr(P.error_flag, 1);
+            }
+            __syncthreads();  // pushes complete before the next pop
+            if (s_top[cur ^ 1] > (int)cap) {  // overflowed: drop the pool (error already flagged)
+                __syncthreads();
+                if (tid == 0) s_top[cur ^ 1] = 0;
+                __syncthreads();
+            }
+        }
+        if (valid) {
+            const V3<R> c = {(R)((double)pl.acc[tid] * kAccInvScale),
+                             (R)((double)pl.acc[kBlock + tid] * kAccInvScale),
+                             (R)((double)pl.acc[2 * kBlock + tid] * kAccInvScale)};
+            store_pixel(P, out_idx, c);
+        }
+        __syncthreads();  // accumulators are re-zeroed for the next tile
+    }
+    flush_counts(k, P.counters);
+}
+
+// De-interleave gathered shard strips into one image.
+__global__ void assemble_shards(const unsigned char* __restrict__ gathered, unsigned char* __restrict__ image,
+                                uint32_t width, uint32_t height, uint32_t shards, uint32_t strip_rows,
+                                uint32_t bpp) {
+    const uint64_t row_bytes = (uint64_t)width * bpp;
+    const uint32_t y = blockIdx.y;
+    if (y >= height) return;
+    const uint32_t trow = y / RT_TILE_H, within = y % RT_TILE_H;
+    const uint32_t shard = trow % shards, local_trow = trow / shards;
+    const uint64_t src_row = (uint64_t)shard * strip_rows + (uint64_t)local_trow * RT_TILE_H + within;
+    const unsigned char* src = gathered + src_row * row_bytes;
+    unsigned char* dst = image + (uint64_t)y * row_bytes;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < row_bytes; i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
+// ------------------------------------------------------------ launchers
+template <typename R>
+hipError_t launch_trace(const LaunchParams<R>& P, bool pool, uint32_t grid, size_t dyn_lds, hipStream_t stream) {
+    if (pool) {
+        hipLaunchKernelGGL(trace_pool<R>, dim3(grid), dim3(kBlock), dyn_lds, stream, P);
+    } else {
+        hipLaunchKernelGGL(trace_direct<R>, dim3(grid), dim3(kBlock), 0, stream, P);
+    }
+    return hipGetLastError();
+}
+
+template <typename R>
+hipError_t occupancy(bool pool, size_t dyn_lds, int* blocks_per_cu) {
+    if (pool)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_pool<R>, kBlock, dyn_lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_direct<R>, kBlock, 0);
+}
+
+template hipError_t launch_trace<float>(const LaunchParams<float>&, bool, uint32_t, size_t, hipStream_t);
+template hipError_t launch_trace<double>(const LaunchParams<double>&, bool, uint32_t, size_t, hipStream_t);
+template hipError_t occupancy<float>(bool, size_t, int*);
+template hipError_t occupancy<double>(bool, size_t, int*);
+
+hipError_t launch_assemble(const void* gathered, void* image, uint32_t width, uint32_t height, uint32_t shards,
+                           uint32_t strip_rows, uint32_t bpp, hipStream_t stream) {
+    dim3 grid(4, height);
+    hipLaunchKernelGGL(assemble_shards, grid, dim3(256), 0, stream, static_cast<const unsigned char*>(gathered),
+                       static_cast<unsigned char*>(image), width, height, shards, strip_rows, bpp);
+    return hipGetLastError();
+}
+
+}  // namespace rtc

@@ -1,0 +1,342 @@
+"""rtc_amd — MI355X-native render path for the Ray Tracer Challenge world model
+of przemo199/ray-tracer-challenge-rs.
+
+Python view of the C-ABI in include/rtc.h / include/rtc_scene.h (librtc.so,
+built from ray-tracer-challenge-rs_amd/csrc).  It mirrors the reference's
+render API:
+
+    load_scene_description(path)   ray-tracer-cli/src/scene_loader.rs:361-367
+    Camera.render / render_parallel ray-tracer/src/composites/camera.rs:79-112
+                                   -> Context.render (the GPU arm)
+    World.color_at                 ray-tracer/src/composites/world.rs:89-95
+                                   -> Context.color_at (batched)
+
+There is no CPU fallback: importing works without a GPU (for the scene
+loader and ABI checks), but every call that renders raises RenderError with
+RT_ERR_NO_DEVICE when no HIP device is usable, and the module refuses to load
+at all when librtc.so is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+__all__ = [
+    "RenderError", "lib_path", "abi_version", "device_count", "matrix_inverse", "camera_make",
+    "camera_resize", "load_scene", "load_scene_text", "SceneTables", "Context", "shard_rows",
+    "RT_DEFAULT_MAX_DEPTH", "RT_TILE_H", "RT_TILE_W",
+]
+
+RT_TILE_W = 16
+RT_TILE_H = 16
+RT_DEFAULT_MAX_DEPTH = 6  # World::MAX_REFLECTION_ITERATIONS, world.rs:15
+RT_MAX_SUPPORTED_DEPTH = 16
+
+RT_OK = 0
+STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_HIP", -3: "RT_ERR_NO_DEVICE", -4: "RT_ERR_NO_SCENE",
+          -5: "RT_ERR_OOM", -6: "RT_ERR_POOL", -7: "RT_ERR_IO"}
+
+SHAPE_KINDS = {"sphere": 0, "plane": 1, "cube": 2, "cylinder": 3, "cone": 4, "triangle": 5}
+PATTERN_KINDS = {"stripe": 0, "gradient": 1, "ring": 2, "checker": 3, "complex": 4, "test": 5}
+PRECISIONS = {"f32": 0, "f64": 1}
+OUT_FORMATS = {"real": 0, "u8": 1}
+
+
+class RenderError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"{STATUS.get(code, code)}: {message}")
+        self.code = code
+
+
+# ----------------------------------------------------------------- structs
+class ShapeDesc(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("material", C.c_int32), ("inverse", C.c_double * 16),
+                ("minimum", C.c_double), ("maximum", C.c_double), ("closed", C.c_int32),
+                ("reserved", C.c_int32), ("vertex_1", C.c_double * 3), ("edge_1", C.c_double * 3),
+                ("edge_2", C.c_double * 3), ("normal", C.c_double * 3)]
+
+
+class MaterialDesc(C.Structure):
+    _fields_ = [("color", C.c_double * 3), ("ambient", C.c_double), ("diffuse", C.c_double),
+                ("specular", C.c_double), ("shininess", C.c_double), ("reflectiveness", C.c_double),
+                ("transparency", C.c_double), ("refractive_index", C.c_double), ("casts_shadow", C.c_int32),
+                ("pattern", C.c_int32)]
+
+
+class PatternDesc(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("sub_a", C.c_int32), ("sub_b", C.c_int32), ("reserved", C.c_int32),
+                ("color_a", C.c_double * 3), ("color_b", C.c_double * 3), ("inverse", C.c_double * 16)]
+
+
+class LightDesc(C.Structure):
+    _fields_ = [("position", C.c_double * 3), ("intensity", C.c_double * 3)]
+
+
+class CameraDesc(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("field_of_view", C.c_double),
+                ("half_width", C.c_double), ("half_height", C.c_double), ("pixel_size", C.c_double),
+                ("inverse", C.c_double * 16), ("origin", C.c_double * 3)]
+
+    def copy(self) -> "CameraDesc":
+        c = CameraDesc()
+        C.pointer(c)[0] = self
+        return c
+
+
+class RenderOptions(C.Structure):
+    _fields_ = [("max_depth", C.c_uint32), ("precision", C.c_uint32), ("out_format", C.c_uint32),
+                ("shard_index", C.c_uint32), ("shard_count", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("primary", C.c_uint64), ("shadow", C.c_uint64), ("reflect", C.c_uint64),
+                ("refract", C.c_uint64), ("shaded", C.c_uint64), ("lit_patterned", C.c_uint64),
+                ("refract_evals", C.c_uint64), ("schlick_evals", C.c_uint64), ("kernel_ms", C.c_double),
+                ("algorithmic_flops", C.c_double)]
+
+    def as_dict(self) -> dict:
+        d = {name: getattr(self, name) for name, _ in self._fields_}
+        d["rays"] = self.primary + self.shadow + self.reflect + self.refract
+        return d
+
+
+class SceneView(C.Structure):
+    _fields_ = [("shapes", C.POINTER(ShapeDesc)), ("n_shapes", C.c_uint32),
+                ("materials", C.POINTER(MaterialDesc)), ("n_materials", C.c_uint32),
+                ("patterns", C.POINTER(PatternDesc)), ("n_patterns", C.c_uint32),
+                ("lights", C.POINTER(LightDesc)), ("n_lights", C.c_uint32),
+                ("camera", CameraDesc), ("duplicate_shapes", C.c_uint32)]
+
+
+# --------------------------------------------------------------- library
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def lib_path() -> str:
+    return os.path.join(_HERE, "_lib", "librtc.so")
+
+
+def _load() -> C.CDLL:
+    path = lib_path()
+    if not os.path.exists(path):
+        raise ImportError(f"rtc_amd: {path} is missing — build it with `python -c 'import __graft_entry__ as g; "
+                          f"g.build()'` (hipcc --offload-arch=gfx950)")
+    lib = C.CDLL(path)
+    P = C.POINTER
+    sig = {
+        "rt_abi_version": (C.c_int, []),
+        "rt_last_error": (C.c_char_p, []),
+        "rt_device_count": (C.c_int, [P(C.c_int)]),
+        "rt_context_create": (C.c_int, [C.c_int, P(C.c_void_p)]),
+        "rt_context_destroy": (C.c_int, [C.c_void_p]),
+        "rt_scene_upload": (C.c_int, [C.c_void_p, P(ShapeDesc), C.c_uint32, P(MaterialDesc), C.c_uint32,
+                                      P(PatternDesc), C.c_uint32, P(LightDesc), C.c_uint32]),
+        "rt_shard_rows": (C.c_int, [C.c_uint32, C.c_uint32, P(C.c_uint32)]),
+        "rt_render": (C.c_int, [C.c_void_p, P(CameraDesc), P(RenderOptions), C.c_void_p, P(Stats)]),
+        "rt_render_device": (C.c_int, [C.c_void_p, P(CameraDesc), P(RenderOptions), C.c_void_p, C.c_void_p]),
+        "rt_color_at": (C.c_int, [C.c_void_p, P(C.c_double), C.c_uint64, C.c_uint32, C.c_uint32, P(C.c_double),
+                                  P(Stats)]),
+        "rt_read_counters": (C.c_int, [C.c_void_p, P(Stats)]),
+        "rt_assemble_shards": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                         C.c_void_p, C.c_void_p]),
+        "rt_scene_load_yaml": (C.c_int, [C.c_char_p, P(C.c_void_p)]),
+        "rt_scene_load_yaml_text": (C.c_int, [C.c_char_p, P(C.c_void_p)]),
+        "rt_scene_view_get": (C.c_int, [C.c_void_p, P(SceneView)]),
+        "rt_scene_free": (None, [C.c_void_p]),
+        "rt_camera_make": (C.c_int, [C.c_uint32, C.c_uint32, C.c_double, P(C.c_double), P(C.c_double),
+                                     P(C.c_double), P(CameraDesc)]),
+        "rt_camera_resize": (C.c_int, [P(CameraDesc), C.c_uint32, C.c_uint32]),
+        "rt_matrix_inverse": (C.c_int, [P(C.c_double), P(C.c_double)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_lib = _load()
+
+# Every symbol include/rtc.h and include/rtc_scene.h declare (checked by tests).
+EXPORTED_SYMBOLS = (
+    "rt_abi_version", "rt_last_error", "rt_device_count", "rt_context_create", "rt_context_destroy",
+    "rt_scene_upload", "rt_shard_rows", "rt_render", "rt_render_device", "rt_color_at", "rt_read_counters",
+    "rt_assemble_shards", "rt_scene_load_yaml", "rt_scene_load_yaml_text", "rt_scene_view_get", "rt_scene_free",
+    "rt_camera_make", "rt_camera_resize", "rt_matrix_inverse",
+)
+
+
+def _check(rc: int) -> None:
+    if rc != RT_OK:
+        raise RenderError(rc, _lib.rt_last_error().decode(errors="replace"))
+
+
+def abi_version() -> int:
+    return _lib.rt_abi_version()
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    _check(_lib.rt_device_count(C.byref(n)))
+    return n.value
+
+
+def matrix_inverse(m) -> np.ndarray:
+    """Matrix<4>::inverse (matrix.rs:247-258) on 16 row-major f64."""
+    a = (C.c_double * 16)(*np.asarray(m, dtype=np.float64).reshape(16))
+    out = (C.c_double * 16)()
+    _check(_lib.rt_matrix_inverse(a, out))
+    return np.array(out[:], dtype=np.float64).reshape(4, 4)
+
+
+def camera_make(width: int, height: int, fov: float, frm, to, up) -> CameraDesc:
+    """Camera::new + set_transformation(view_transform(from, to, up))."""
+    cam = CameraDesc()
+    v = lambda x: (C.c_double * 3)(*[float(t) for t in x])  # noqa: E731
+    _check(_lib.rt_camera_make(width, height, float(fov), v(frm), v(to), v(up), C.byref(cam)))
+    return cam
+
+
+def camera_resize(cam: CameraDesc, width: int, height: int) -> CameraDesc:
+    """Camera::new for another canvas size, same fov/transform (= editing YAML width/height)."""
+    c = cam.copy()
+    _check(_lib.rt_camera_resize(C.byref(c), width, height))
+    return c
+
+
+def shard_rows(height: int, shard_count: int) -> int:
+    r = C.c_uint32(0)
+    _check(_lib.rt_shard_rows(height, shard_count, C.byref(r)))
+    return r.value
+
+
+@dataclass
+class SceneTables:
+    """Flattened world: the POD tables rt_scene_upload takes, plus the camera."""
+    shapes: C.Array
+    materials: C.Array
+    patterns: C.Array
+    lights: C.Array
+    camera: CameraDesc
+    duplicate_shapes: int = 0
+
+    @property
+    def counts(self):
+        return len(self.shapes), len(self.materials), len(self.patterns), len(self.lights)
+
+    def args(self):
+        """(shapes, n, materials, n, patterns, n, lights, n) for C calls."""
+        return (self.shapes, len(self.shapes), self.materials, len(self.materials), self.patterns,
+                len(self.patterns), self.lights, len(self.lights))
+
+    def has_secondary(self) -> bool:
+        return any(m.reflectiveness != 0.0 or m.transparency != 0.0 for m in self.materials)
+
+
+def _tables_from_view(v: SceneView) -> SceneTables:
+    def copy(ptr, n, typ):
+        arr = (typ * n)()
+        if n:
+            C.memmove(arr, ptr, n * C.sizeof(typ))
+        return arr
+    return SceneTables(copy(v.shapes, v.n_shapes, ShapeDesc), copy(v.materials, v.n_materials, MaterialDesc),
+                       copy(v.patterns, v.n_patterns, PatternDesc), copy(v.lights, v.n_lights, LightDesc),
+                       v.camera.copy(), v.duplicate_shapes)
+
+
+def _load_with(fn, arg: bytes) -> SceneTables:
+    h = C.c_void_p()
+    _check(fn(arg, C.byref(h)))
+    try:
+        v = SceneView()
+        _check(_lib.rt_scene_view_get(h, C.byref(v)))
+        return _tables_from_view(v)
+    finally:
+        _lib.rt_scene_free(h)
+
+
+def load_scene(path: str) -> SceneTables:
+    """load_scene_description (scene_loader.rs:361-367): YAML file -> tables + camera."""
+    return _load_with(_lib.rt_scene_load_yaml, os.fsencode(path))
+
+
+def load_scene_text(text: str) -> SceneTables:
+    return _load_with(_lib.rt_scene_load_yaml_text, text.encode())
+
+
+class Context:
+    """One GPU.  Mirrors the borrow in Camera::render(&self, world: &World)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        _check(_lib.rt_context_create(device, C.byref(h)))
+        self._h = h
+        self.device = device
+        self.scene: SceneTables | None = None
+
+    def close(self) -> None:
+        if self._h:
+            _lib.rt_context_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, scene: SceneTables) -> None:
+        _check(_lib.rt_scene_upload(self._h, *scene.args()))
+        self.scene = scene
+
+    @staticmethod
+    def options(depth=RT_DEFAULT_MAX_DEPTH, precision="f32", out_format="real", shard=(0, 1)) -> RenderOptions:
+        return RenderOptions(depth, PRECISIONS[precision], OUT_FORMATS[out_format], shard[0], shard[1], 0)
+
+    def render(self, camera: CameraDesc, depth: int = RT_DEFAULT_MAX_DEPTH, precision: str = "f32",
+               out_format: str = "real", shard=(0, 1)):
+        """Render one frame (or one shard's strip) into a host array (H, W, 3); returns (image, stats)."""
+        opts = self.options(depth, precision, out_format, shard)
+        rows = camera.height if shard[1] == 1 else shard_rows(camera.height, shard[1])
+        dtype = np.uint8 if out_format == "u8" else (np.float32 if precision == "f32" else np.float64)
+        img = np.zeros((rows, camera.width, 3), dtype=dtype)
+        st = Stats()
+        _check(_lib.rt_render(self._h, C.byref(camera), C.byref(opts), img.ctypes.data_as(C.c_void_p),
+                              C.byref(st)))
+        return img, st.as_dict()
+
+    def render_device(self, camera: CameraDesc, out_ptr: int, stream_ptr: int | None = None,
+                      depth: int = RT_DEFAULT_MAX_DEPTH, precision: str = "f32", out_format: str = "real",
+                      shard=(0, 1)) -> None:
+        """Asynchronous render into a device buffer (e.g. a torch tensor's data_ptr()) on a HIP stream."""
+        opts = self.options(depth, precision, out_format, shard)
+        _check(_lib.rt_render_device(self._h, C.byref(camera), C.byref(opts), C.c_void_p(out_ptr),
+                                     C.c_void_p(stream_ptr or 0)))
+
+    def color_at(self, rays, depth: int = RT_DEFAULT_MAX_DEPTH, precision: str = "f32"):
+        """Batched World::color_at: rays (n, 6) = origin, direction -> colours (n, 3) f64."""
+        r = np.ascontiguousarray(np.asarray(rays, dtype=np.float64).reshape(-1, 6))
+        out = np.zeros((r.shape[0], 3), dtype=np.float64)
+        st = Stats()
+        _check(_lib.rt_color_at(self._h, r.ctypes.data_as(C.POINTER(C.c_double)), r.shape[0], depth,
+                                PRECISIONS[precision], out.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st)))
+        return out, st.as_dict()
+
+    def counters(self) -> dict:
+        st = Stats()
+        _check(_lib.rt_read_counters(self._h, C.byref(st)))
+        return st.as_dict()
+
+    def assemble_shards(self, gathered_ptr: int, width: int, height: int, shards: int, bytes_per_pixel: int,
+                        image_ptr: int, stream_ptr: int | None = None) -> None:
+        _check(_lib.rt_assemble_shards(self._h, C.c_void_p(gathered_ptr), width, height, shards, bytes_per_pixel,
+                                       C.c_void_p(image_ptr), C.c_void_p(stream_ptr or 0)))
