@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--mode", choices=["frames", "tiled"], default="frames")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--flags", type=int, default=0, help="RT_FLAG_* diagnostic ablations (profiling only)")
     return ap.parse_args()
 
 
@@ -124,7 +125,7 @@ def main():
     shard = (rank, world) if tiled else (0, 1)
 
     def step():
-        ctx.render_device(cam, out.data_ptr(), sptr, args.depth, args.precision, "real", shard)
+        ctx.render_device(cam, out.data_ptr(), sptr, args.depth, args.precision, "real", shard, args.flags)
         if tiled:
             chunks = list(gathered.chunk(world)) if rank == 0 else None
             dist.gather(out, chunks, dst=0)

@@ -151,13 +151,19 @@ typedef struct rt_camera_desc {
     double origin[3];   /* inverse * Point::ORIGIN (camera.rs:114-116)  */
 } rt_camera_desc;
 
+/* Diagnostic ablation flags (profiling only; outputs are wrong with them). */
+#define RT_FLAG_NO_COUNTERS 1u /* skip the per-workgroup counter flush      */
+#define RT_FLAG_NO_SHADE 2u    /* closest hit only, colour = normalised t   */
+#define RT_FLAG_NO_TRACE 4u    /* camera ray only, colour = direction       */
+
 typedef struct rt_render_options {
     uint32_t max_depth;    /* `remaining` of the primary ray; 6 = reference */
     uint32_t precision;    /* rt_precision                                  */
     uint32_t out_format;   /* rt_out_format                                 */
     uint32_t shard_index;  /* row-block sharding            */
     uint32_t shard_count;  /* 1 = the whole image                           */
-    uint32_t flags;        /* reserved, 0                                   */
+    uint32_t flags;        /* 0; RT_FLAG_* diagnostic ablations (never in  */
+                           /* a parity or benchmark result)                */
 } rt_render_options;
 
 /* Ray counts in the reference's semantics plus the terms of
@@ -204,7 +210,8 @@ int rt_render(rt_context* ctx, const rt_camera_desc* camera,
               rt_stats* stats);
 
 /* Asynchronous render into a caller-owned DEVICE buffer on `hip_stream`
- * (a hipStream_t, NULL = the context's own stream).  No host sync. */
+ * (a hipStream_t; NULL = HIP's default stream).  No host sync.  The caller's
+ * HIP runtime must be the one librtc is bound to (one runtime per process). */
 int rt_render_device(rt_context* ctx, const rt_camera_desc* camera,
                      const rt_render_options* options, void* out_device,
                      void* hip_stream);

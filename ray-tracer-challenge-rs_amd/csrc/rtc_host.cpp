@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -72,13 +73,17 @@ struct rt_context {
     hipStream_t stream = nullptr;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     unsigned long long* d_tile_counter = nullptr;
-    unsigned long long tile_base = 0;
+    unsigned long long tile_base[rtc::kTileQueues] = {};
     unsigned long long* d_counters = nullptr;  // kNumCounters cumulative
     int32_t* d_error = nullptr;
     bool have_scene = false;
     rtc::DeviceWorld<float> w32;
     rtc::DeviceWorld<double> w64;
     rtc::FlopScene flops;  // per-kind shape counts for the algorithmic FLOP model
+    bool persistent_direct = false;  // scheduling of each kernel (RTC_SCHED_DIRECT / RTC_SCHED_POOL)
+    bool persistent_pool = true;
+    size_t occ_lds[4] = {0, 0, 0, 0};  // occupancy cache: {direct,pool} x {f32,f64}
+    int occ_blocks[4] = {0, 0, 0, 0};
     void* d_scratch = nullptr;  // host-buffer renders / color_at staging
     size_t scratch_bytes = 0;
 };
@@ -219,6 +224,7 @@ constexpr size_t kMaxLds = 160 * 1024 - 1024;  // leave room for static LDS
 
 struct LaunchShape {
     bool pool;
+    bool persistent;
     uint32_t grid;
     size_t lds;
     uint32_t cap, batch;
@@ -238,18 +244,26 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
         ls.cap = pool_capacity(depth, batch);
         ls.lds = pool_lds_bytes<R>(ls.cap);
     }
+    const int key = (ls.pool ? 1 : 0) + (sizeof(R) == 8 ? 2 : 0);
     int per_cu = 0;
-    RT_HIP(occupancy<R>(ls.pool, ls.lds, &per_cu));
+    if (ctx->occ_lds[key] == ls.lds && ctx->occ_blocks[key] > 0) {
+        per_cu = ctx->occ_blocks[key];
+    } else {
+        RT_HIP(occupancy<R>(ls.pool, ls.lds, &per_cu));
+        ctx->occ_lds[key] = ls.lds;
+        ctx->occ_blocks[key] = per_cu;
+    }
     if (per_cu < 1) per_cu = 1;
     const uint64_t resident = (uint64_t)per_cu * (uint64_t)ctx->cu_count;
-    ls.grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, resident));
+    ls.persistent = ls.pool ? ctx->persistent_pool : ctx->persistent_direct;
+    ls.grid = ls.persistent ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, resident)) : n_tiles;
     return RT_OK;
 }
 
 template <typename R>
 int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const double* d_rays, uint64_t n_rays,
            uint32_t depth, uint32_t out_format, uint32_t shard_index, uint32_t shard_count, void* out_device,
-           hipStream_t stream) {
+           hipStream_t stream, uint32_t flags = 0) {
     LaunchParams<R> P{};
     P.scene = w.scene;
     if (cam) {
@@ -282,9 +296,22 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     if (rc) return rc;
     P.pool_capacity = ls.cap;
     P.pop_batch = ls.batch;
-    P.tile_base = ctx->tile_base;
-    // every launched workgroup makes exactly one failing dequeue at the end
-    ctx->tile_base += (unsigned long long)P.n_tiles + ls.grid;
+    P.persistent = ls.persistent ? 1 : 0;
+    P.dequeue_chunk = ls.pool ? kDequeueChunkPool : kDequeueChunkDirect;
+    P.flags = flags;
+    // Queue q holds tiles q, q+8, ... and serves workgroups q, q+8, ....  The
+    // atomics one launch makes on queue q: one per chunk handed out, plus one
+    // failing fetch per workgroup — except the workgroup that ends inside a
+    // partial last chunk, which stops without fetching again.
+    for (int q = 0; q < kTileQueues && ls.persistent; ++q) {
+        P.tile_base[q] = ctx->tile_base[q];
+        const uint64_t C = P.dequeue_chunk;
+        const uint64_t tiles_q = P.n_tiles > (uint32_t)q ? (P.n_tiles - q + kTileQueues - 1) / kTileQueues : 0;
+        const uint64_t chunks_q = (tiles_q + C - 1) / C;
+        const uint64_t blocks_q = ls.grid > (uint32_t)q ? (ls.grid - q + kTileQueues - 1) / kTileQueues : 0;
+        const uint64_t partial_q = (tiles_q % C) != 0 ? 1 : 0;
+        ctx->tile_base[q] += chunks_q + blocks_q - partial_q;
+    }
     RT_HIP(launch_trace<R>(P, ls.pool, ls.grid, ls.lds, stream));
     return RT_OK;
 }
@@ -315,7 +342,12 @@ int ensure_scratch(rt_context* ctx, size_t bytes) {
 }
 
 int read_counters(rt_context* ctx, unsigned long long out[kNumCounters]) {
-    RT_HIP(hipMemcpy(out, ctx->d_counters, kNumCounters * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> shards((size_t)kCounterShards * kNumCounters);
+    RT_HIP(hipMemcpy(shards.data(), ctx->d_counters, shards.size() * sizeof(unsigned long long),
+                     hipMemcpyDeviceToHost));
+    for (int i = 0; i < kNumCounters; ++i) out[i] = 0;
+    for (int s = 0; s < kCounterShards; ++s)
+        for (int i = 0; i < kNumCounters; ++i) out[i] += shards[(size_t)s * kNumCounters + i];
     return RT_OK;
 }
 
@@ -377,13 +409,18 @@ int rt_context_create(int device_ordinal, rt_context** out) {
     hipDeviceProp_t prop;
     RT_HIP(hipGetDeviceProperties(&prop, device_ordinal));
     ctx->cu_count = prop.multiProcessorCount;
+    // scheduling knobs: "persistent" (resident grid + per-XCD tile queues) or
+    // "grid" (one workgroup per tile, the hardware dispatcher balances)
+    if (const char* e = std::getenv("RTC_SCHED_DIRECT")) ctx->persistent_direct = std::strcmp(e, "persistent") == 0;
+    if (const char* e = std::getenv("RTC_SCHED_POOL")) ctx->persistent_pool = std::strcmp(e, "grid") != 0;
     RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreate(&ctx->ev_start));
     RT_HIP(hipEventCreate(&ctx->ev_stop));
-    RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_tile_counter), sizeof(unsigned long long)));
-    RT_HIP(hipMemset(ctx->d_tile_counter, 0, sizeof(unsigned long long)));
-    RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_counters), kNumCounters * sizeof(unsigned long long)));
-    RT_HIP(hipMemset(ctx->d_counters, 0, kNumCounters * sizeof(unsigned long long)));
+    RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_tile_counter), kTileQueues * sizeof(unsigned long long)));
+    RT_HIP(hipMemset(ctx->d_tile_counter, 0, kTileQueues * sizeof(unsigned long long)));
+    const size_t counter_bytes = (size_t)kCounterShards * kNumCounters * sizeof(unsigned long long);
+    RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_counters), counter_bytes));
+    RT_HIP(hipMemset(ctx->d_counters, 0, counter_bytes));
     RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_error), sizeof(int32_t)));
     RT_HIP(hipMemset(ctx->d_error, 0, sizeof(int32_t)));
     *out = ctx.release();
@@ -442,12 +479,12 @@ int rt_render_device(rt_context* ctx, const rt_camera_desc* cam, const rt_render
     if (!cam || !out_device) return set_error(RT_ERR_INVALID, "null camera or output");
     if (cam->width == 0 || cam->height == 0) return RT_OK;  // empty canvas (canvas.rs:27-35)
     RT_HIP(hipSetDevice(ctx->device));
-    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);  // NULL = HIP's default stream
     if (o->precision == RT_PRECISION_F32)
         return launch<float>(ctx, ctx->w32, cam, nullptr, 0, o->max_depth, o->out_format, o->shard_index,
-                             o->shard_count, out_device, s);
+                             o->shard_count, out_device, s, o->flags);
     return launch<double>(ctx, ctx->w64, cam, nullptr, 0, o->max_depth, o->out_format, o->shard_index,
-                          o->shard_count, out_device, s);
+                          o->shard_count, out_device, s, o->flags);
 }
 
 int rt_render(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, void* out_host,
@@ -470,7 +507,7 @@ int rt_render(rt_context* ctx, const rt_camera_desc* cam, const rt_render_option
     unsigned long long before[kNumCounters], after[kNumCounters];
     if ((rc = read_counters(ctx, before))) return rc;
     RT_HIP(hipEventRecord(ctx->ev_start, ctx->stream));
-    if ((rc = rt_render_device(ctx, cam, o, ctx->d_scratch, ctx->stream))) return rc;
+    if ((rc = rt_render_device(ctx, cam, o, ctx->d_scratch, static_cast<void*>(ctx->stream)))) return rc;
     RT_HIP(hipEventRecord(ctx->ev_stop, ctx->stream));
     RT_HIP(hipStreamSynchronize(ctx->stream));
     float ms = 0.f;
@@ -546,7 +583,7 @@ int rt_assemble_shards(rt_context* ctx, const void* gathered, uint32_t width, ui
     RT_HIP(hipSetDevice(ctx->device));
     uint32_t rows = 0;
     rt_shard_rows(height, shards, &rows);
-    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);  // NULL = HIP's default stream
     RT_HIP(launch_assemble(gathered, image, width, height, shards, rows, bpp, s));
     return RT_OK;
 }

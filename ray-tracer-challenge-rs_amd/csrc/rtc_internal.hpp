@@ -27,6 +27,18 @@ constexpr int kTilePixels = RT_TILE_W * RT_TILE_H;  // one tile per workgroup pa
 static_assert(kTilePixels == kBlock, "one pixel per thread per tile");
 constexpr int kNumKinds = 6;
 constexpr int kNumCounters = 8;    // order of rt_stats' first eight fields
+// Event counters are sharded: workgroup b adds into shard b % kCounterShards
+// (same-address global atomics from every workgroup cost ~66 us per 1080p
+// frame on MI355X; sharded they are noise).  The host sums the shards.
+constexpr int kCounterShards = 256;
+// Tile queues: one atomic head saturates at ~88 dequeues/us on MI355X
+// (MI355X_MICROARCH.md, price list row "dequeue"), i.e. ~93 us for the 8160
+// tiles of a 1920x1080 frame.  Tile t lives in queue t % 8 and workgroup b
+// pulls from queue b % 8 (blocks b and b+8 share an XCD under round-robin
+// dispatch; placement only affects speed).
+constexpr int kTileQueues = 8;
+constexpr int kDequeueChunkDirect = 4;  // tiles per dequeue: cheap, uniform tiles
+constexpr int kDequeueChunkPool = 1;    // costly, high-variance tiles: balance first
 
 // Fixed-point pixel accumulator of the pool kernel: contributions are summed
 // as int64 multiples of 2^-48 so the per-pixel sum is independent of the
@@ -106,9 +118,12 @@ struct LaunchParams {
     uint32_t max_depth;      // `remaining` of the primary ray
     uint32_t pool_capacity;  // pool kernel: rays held in LDS
     uint32_t pop_batch;      // pool kernel: rays popped per iteration (<= kBlock)
-    unsigned long long* tile_counter;  // cumulative dequeue counter
-    unsigned long long tile_base;      // its value at this launch's start
-    unsigned long long* counters;      // kNumCounters cumulative u64
+    uint32_t persistent;     // 1: resident grid dequeues tiles; 0: one workgroup per tile
+    uint32_t dequeue_chunk;  // tiles per dequeue (persistent mode)
+    uint32_t flags;          // RT_FLAG_* diagnostic ablations
+    unsigned long long* tile_counter;  // kTileQueues cumulative dequeue counters (one per XCD)
+    unsigned long long tile_base[kTileQueues];  // their values at this launch's start
+    unsigned long long* counters;      // kCounterShards x kNumCounters cumulative u64
     int32_t* error_flag;               // set nonzero on pool overflow
 };
 

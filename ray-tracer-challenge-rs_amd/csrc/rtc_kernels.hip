@@ -215,11 +215,25 @@ __device__ inline void entries(const ShapeRec<R>& s, V3<R> o, V3<R> d, F&& emit)
     if constexpr (K == RT_SHAPE_SPHERE) {  // sphere.rs:41-53
         const R a = dot(d, d);
         const R b = (R)2 * dot(d, o);
-        const R c = dot(o, o) - (R)1;
-        quadratic<R>(a, b, c, [&](R t1, R t2) {
-            emit(t1);
-            emit(t2);
-        });
+        if constexpr (sizeof(R) == 4) {
+            // b^2 - 4ac == 4 (a - |d x o|^2) (Lagrange's identity).  The
+            // textbook form cancels catastrophically in f32 when the local
+            // origin is far from the unit sphere (e.g. the backdrop of
+            // shadow_puppets.yaml, a sphere scaled by 0.01 in z).
+            const V3<R> c = cross(d, o);
+            const R disc = (R)4 * (a - dot(c, c));
+            if (disc < (R)0) return;
+            const R root = T::sqrt(disc);
+            const R ri = __builtin_amdgcn_rcpf((R)2 * a);
+            emit((-b - root) * ri);
+            emit((-b + root) * ri);
+        } else {
+            const R c = dot(o, o) - (R)1;
+            quadratic<R>(a, b, c, [&](R t1, R t2) {
+                emit(t1);
+                emit(t2);
+            });
+        }
     } else if constexpr (K == RT_SHAPE_PLANE) {  // plane.rs:42-48
         if (T::fabs(d.y) < T::kEps) return;
         emit(T::div(-o.y, d.y));
@@ -316,11 +330,23 @@ __device__ inline void entries(const ShapeRec<R>& s, V3<R> o, V3<R> d, F&& emit)
     }
 }
 
+// Copy a wave-uniform record.  The world tables reach the kernels as
+// `const T* __restrict__` parameters (see scene_view): LLVM can then prove no
+// store of the launch clobbers them and selects scalar s_load_dwordxN into
+// SGPRs (free VALU operands) instead of per-lane global_loads.
+template <typename T>
+__device__ inline T ld_uniform(const T* p) {
+    return *p;
+}
+
 // Visit every shape of kind K (wave-uniform loop, scalar loads).
 template <typename R, int K, typename F>
 __device__ inline void for_kind(const DevScene<R>& sc, F&& f) {
     const int b = sc.kind_begin[K], e = sc.kind_begin[K + 1];
-    for (int i = b; i < e; ++i) f(sc.shapes[i], i);
+    for (int i = b; i < e; ++i) {
+        const ShapeRec<R> s = ld_uniform(&sc.shapes[i]);
+        f(s, i);
+    }
 }
 
 template <typename R, typename F>
@@ -550,7 +576,7 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
     if (patterned) base = pattern_color(sc, m.pattern, s, over);
     V3<R> surface = {(R)0, (R)0, (R)0};
     for (int li = 0; li < sc.n_lights; ++li) {
-        const LightRec<R>& L = sc.lights[li];
+        const LightRec<R> L = ld_uniform(&sc.lights[li]);
         const V3<R> lpos = {L.position[0], L.position[1], L.position[2]};
         const V3<R> to_light = vsub(lpos, over);
         const R dist = magnitude(to_light);
@@ -578,7 +604,10 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
     }
     out.surface = surface;
     out.refl_child = out.refr_child = false;
-    if constexpr (kChildren) {
+    if constexpr (!kChildren) {
+        // shade_hit evaluates Schlick whenever the material is both (world.rs:59-60)
+        if (m.reflectiveness > (R)0 && m.transparency > (R)0) k.c[7]++;
+    } else {
         const bool reflective = m.reflectiveness > (R)0, transparent = m.transparency > (R)0;
         R n1 = (R)1, n2 = (R)1;
         if (m.transparency != (R)0) refractive_indices(sc, o, d, h, n1, n2);
@@ -712,17 +741,56 @@ __device__ inline void flush_counts(const Counts& k, unsigned long long* global)
         if ((threadIdx.x & 63) == 0 && v) atomicAdd(&s_counts[i], v);
     }
     __syncthreads();
-    if (threadIdx.x < kNumCounters && s_counts[threadIdx.x]) atomicAdd(&global[threadIdx.x], s_counts[threadIdx.x]);
+    if (threadIdx.x < kNumCounters && s_counts[threadIdx.x])
+        atomicAdd(&global[(blockIdx.x % kCounterShards) * kNumCounters + threadIdx.x], s_counts[threadIdx.x]);
 }
+
+// Next tile of this workgroup (called by thread 0 only; `chunk`/`pos` live in
+// its registers).  Persistent mode pulls kDequeueChunk consecutive tiles of
+// its queue (see kTileQueues) per returning atomic, so the ~1-3 us atomic
+// round trip is paid once per chunk, not per tile.
+template <typename R>
+__device__ inline unsigned int next_tile(const LaunchParams<R>& P, uint32_t it, unsigned long long& chunk,
+                                         uint32_t& pos) {
+    if (!P.persistent) return it == 0 ? blockIdx.x : 0xFFFFFFFFu;  // grid = one workgroup per tile
+    const uint32_t q = blockIdx.x % kTileQueues;
+    if (it == 0 || pos == P.dequeue_chunk) {
+        chunk = atomicAdd(&P.tile_counter[q], 1ull) - P.tile_base[q];
+        pos = 0;
+    }
+    const unsigned long long t = q + (unsigned long long)kTileQueues * (chunk * P.dequeue_chunk + pos++);
+    return t < P.n_tiles ? (unsigned int)t : 0xFFFFFFFFu;
+}
+
+// The world as seen by one launch, rebuilt from the restrict parameters.
+template <typename R>
+__device__ inline DevScene<R> scene_view(const LaunchParams<R>& P, const ShapeRec<R>* __restrict__ shapes,
+                                         const MaterialRec<R>* __restrict__ materials,
+                                         const PatternRec<R>* __restrict__ patterns,
+                                         const LightRec<R>* __restrict__ lights) {
+    DevScene<R> sc = P.scene;
+    sc.shapes = shapes;
+    sc.materials = materials;
+    sc.patterns = patterns;
+    sc.lights = lights;
+    return sc;
+}
+
+#define RTC_WORLD_PARAMS(R)                                                                                  \
+    const ShapeRec<R>* __restrict__ shapes, const MaterialRec<R>* __restrict__ materials,                   \
+        const PatternRec<R>* __restrict__ patterns, const LightRec<R>* __restrict__ lights
 
 // --------------------------------------------------------------- kernels
 template <typename R>
-__global__ __launch_bounds__(kBlock) void trace_direct(LaunchParams<R> P) {
+__global__ __launch_bounds__(kBlock) void trace_direct(LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
+    const DevScene<R> sc = scene_view(P, shapes, materials, patterns, lights);
     __shared__ unsigned int s_tile[2];
     Counts k = {};
     const uint32_t tid = threadIdx.x;
+    unsigned long long chunk = 0;
+    uint32_t pos = 0;
     for (uint32_t it = 0;; ++it) {
-        if (tid == 0) s_tile[it & 1] = (unsigned int)(atomicAdd(P.tile_counter, 1ull) - P.tile_base);
+        if (tid == 0) s_tile[it & 1] = next_tile(P, it, chunk, pos);
         __syncthreads();
         const uint32_t t = s_tile[it & 1];
         if (t >= P.n_tiles) break;
@@ -734,10 +802,19 @@ __global__ __launch_bounds__(kBlock) void trace_direct(LaunchParams<R> P) {
         k.c[0]++;
         Shaded<R> sh;
         V3<R> c = {(R)0, (R)0, (R)0};
-        if (shade_ray<R, false>(P.scene, o, d, 0, sh, k)) c = sh.surface;
+        if (P.flags & (RT_FLAG_NO_SHADE | RT_FLAG_NO_TRACE)) {
+            if (P.flags & RT_FLAG_NO_TRACE) {
+                c = d;
+            } else {
+                const Hit<R> h = closest_hit(sc, o, d);
+                c = {h.t * (R)0.01, (R)h.slot, (R)0};
+            }
+        } else if (shade_ray<R, false>(sc, o, d, 0, sh, k)) {
+            c = sh.surface;
+        }
         store_pixel(P, out_idx, c);
     }
-    flush_counts(k, P.counters);
+    if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
 }
 
 // Ray pool layout in dynamic LDS: [acc: 3 x kBlock i64][ox oy oz dx dy dz w : cap x R][meta : cap x u32]
@@ -779,7 +856,8 @@ __device__ inline void acc_add(long long* acc, uint32_t pix, double v) {
 }
 
 template <typename R>
-__global__ __launch_bounds__(kBlock) void trace_pool(LaunchParams<R> P) {
+__global__ __launch_bounds__(kBlock) void trace_pool(LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
+    const DevScene<R> sc = scene_view(P, shapes, materials, patterns, lights);
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ unsigned int s_tile[2];
     __shared__ int s_top[2];
@@ -798,9 +876,11 @@ __global__ __launch_bounds__(kBlock) void trace_pool(LaunchParams<R> P) {
 
     Counts k = {};
     const uint32_t tid = threadIdx.x;
+    unsigned long long chunk = 0;
+    uint32_t pos = 0;
     for (uint32_t it = 0;; ++it) {
         if (tid == 0) {
-            s_tile[it & 1] = (unsigned int)(atomicAdd(P.tile_counter, 1ull) - P.tile_base);
+            s_tile[it & 1] = next_tile(P, it, chunk, pos);
             s_top[0] = 0;
         }
         for (int c = 0; c < 3; ++c) pl.acc[c * kBlock + tid] = 0;
@@ -838,7 +918,7 @@ __global__ __launch_bounds__(kBlock) void trace_pool(LaunchParams<R> P) {
             __syncthreads();  // every lane holds its ray; the next top is set
             Shaded<R> sh;
             bool hit = false;
-            if (active) hit = shade_ray<R, true>(P.scene, ro, rd, meta >> 8, sh, k);
+            if (active) hit = shade_ray<R, true>(sc, ro, rd, meta >> 8, sh, k);
             const uint32_t pix = meta & 0xFFu;
             if (hit) {
                 acc_add(pl.acc, pix, (double)(sh.surface.x * rw));
@@ -872,7 +952,7 @@ __global__ __launch_bounds__(kBlock) void trace_pool(LaunchParams<R> P) {
         }
         __syncthreads();  // accumulators are re-zeroed for the next tile
     }
-    flush_counts(k, P.counters);
+    if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
 }
 
 // De-interleave gathered shard strips into one image.
@@ -895,9 +975,11 @@ __global__ void assemble_shards(const unsigned char* __restrict__ gathered, unsi
 template <typename R>
 hipError_t launch_trace(const LaunchParams<R>& P, bool pool, uint32_t grid, size_t dyn_lds, hipStream_t stream) {
     if (pool) {
-        hipLaunchKernelGGL(trace_pool<R>, dim3(grid), dim3(kBlock), dyn_lds, stream, P);
+        hipLaunchKernelGGL(trace_pool<R>, dim3(grid), dim3(kBlock), dyn_lds, stream, P, P.scene.shapes,
+                           P.scene.materials, P.scene.patterns, P.scene.lights);
     } else {
-        hipLaunchKernelGGL(trace_direct<R>, dim3(grid), dim3(kBlock), 0, stream, P);
+        hipLaunchKernelGGL(trace_direct<R>, dim3(grid), dim3(kBlock), 0, stream, P, P.scene.shapes,
+                           P.scene.materials, P.scene.patterns, P.scene.lights);
     }
     return hipGetLastError();
 }

@@ -121,6 +121,14 @@ def lib_path() -> str:
 
 def _load() -> C.CDLL:
     path = lib_path()
+    # torch-ROCm bundles its own HIP runtime with the same soname
+    # (libamdhip64.so.7) as /opt/rocm's.  Load it first so librtc binds to the
+    # SAME runtime: torch streams, events and allocations are then valid
+    # handles for the C-ABI (one HIP runtime per process).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(path):
         raise ImportError(f"rtc_amd: {path} is missing — build it with `python -c 'import __graft_entry__ as g; "
                           f"g.build()'` (hipcc --offload-arch=gfx950)")
@@ -299,8 +307,9 @@ class Context:
         self.scene = scene
 
     @staticmethod
-    def options(depth=RT_DEFAULT_MAX_DEPTH, precision="f32", out_format="real", shard=(0, 1)) -> RenderOptions:
-        return RenderOptions(depth, PRECISIONS[precision], OUT_FORMATS[out_format], shard[0], shard[1], 0)
+    def options(depth=RT_DEFAULT_MAX_DEPTH, precision="f32", out_format="real", shard=(0, 1),
+                flags: int = 0) -> RenderOptions:
+        return RenderOptions(depth, PRECISIONS[precision], OUT_FORMATS[out_format], shard[0], shard[1], flags)
 
     def render(self, camera: CameraDesc, depth: int = RT_DEFAULT_MAX_DEPTH, precision: str = "f32",
                out_format: str = "real", shard=(0, 1)):
@@ -316,9 +325,10 @@ class Context:
 
     def render_device(self, camera: CameraDesc, out_ptr: int, stream_ptr: int | None = None,
                       depth: int = RT_DEFAULT_MAX_DEPTH, precision: str = "f32", out_format: str = "real",
-                      shard=(0, 1)) -> None:
-        """Asynchronous render into a device buffer (e.g. a torch tensor's data_ptr()) on a HIP stream."""
-        opts = self.options(depth, precision, out_format, shard)
+                      shard=(0, 1), flags: int = 0) -> None:
+        """Asynchronous render into a device buffer (e.g. a torch tensor's data_ptr()) on a HIP stream
+        (stream_ptr None/0 = HIP's default stream, which is torch's default stream)."""
+        opts = self.options(depth, precision, out_format, shard, flags)
         _check(_lib.rt_render_device(self._h, C.byref(camera), C.byref(opts), C.c_void_p(out_ptr),
                                      C.c_void_p(stream_ptr or 0)))
 
