@@ -31,6 +31,8 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ray-tracer-challenge-rs_amd"))
+# kernel arguments in device memory (see rtc_amd/__init__.py); before HIP starts
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
 PEAK_HBM_GBS = 8000.0

@@ -39,9 +39,11 @@ extern "C" {
 
 #define RT_ABI_VERSION 1
 
-/* Image tile rendered by one workgroup; also the row-block unit of shards. */
-#define RT_TILE_W 16
-#define RT_TILE_H 16
+/* Image tile rendered by one workgroup (one wave = one 64-pixel row run, so
+ * output stores are contiguous); RT_TILE_H rows are also the row-block unit
+ * of shards. */
+#define RT_TILE_W 64
+#define RT_TILE_H 4
 
 /* World::MAX_REFLECTION_ITERATIONS, ray-tracer/src/composites/world.rs:15 */
 #define RT_DEFAULT_MAX_DEPTH 6
@@ -155,6 +157,7 @@ typedef struct rt_camera_desc {
 #define RT_FLAG_NO_COUNTERS 1u /* skip the per-workgroup counter flush      */
 #define RT_FLAG_NO_SHADE 2u    /* closest hit only, colour = normalised t   */
 #define RT_FLAG_NO_TRACE 4u    /* camera ray only, colour = direction       */
+#define RT_FLAG_STAMPS 8u      /* record per-workgroup start/end timestamps */
 
 typedef struct rt_render_options {
     uint32_t max_depth;    /* `remaining` of the primary ray; 6 = reference */
@@ -221,6 +224,10 @@ int rt_render_device(rt_context* ctx, const rt_camera_desc* camera,
 int rt_color_at(rt_context* ctx, const double* rays, uint64_t n_rays,
                 uint32_t max_depth, uint32_t precision, double* out_rgb,
                 rt_stats* stats);
+
+/* Diagnostics: the per-workgroup {start, end} s_memrealtime stamps (100 MHz)
+ * of the last launch made with RT_FLAG_STAMPS; *n = number of workgroups. */
+int rt_debug_stamps(rt_context* ctx, uint64_t* out, uint32_t max_workgroups, uint32_t* n);
 
 /* Cumulative device counters since context creation (after a sync). */
 int rt_read_counters(rt_context* ctx, rt_stats* totals);

@@ -25,7 +25,7 @@ namespace rtc {
 template <typename R>
 hipError_t launch_trace(const LaunchParams<R>& P, bool pool, uint32_t grid, size_t dyn_lds, hipStream_t stream);
 template <typename R>
-hipError_t occupancy(bool pool, size_t dyn_lds, int* blocks_per_cu);
+hipError_t occupancy(bool pool, bool lds, size_t dyn_lds, int* blocks_per_cu);
 hipError_t launch_assemble(const void* gathered, void* image, uint32_t width, uint32_t height, uint32_t shards,
                            uint32_t strip_rows, uint32_t bpp, hipStream_t stream);
 
@@ -52,8 +52,11 @@ struct DeviceWorld {
     MaterialRec<R>* materials = nullptr;
     PatternRec<R>* patterns = nullptr;
     LightRec<R>* lights = nullptr;
+    int32_t* world_slot = nullptr;
     DevScene<R> scene{};
     void release() {
+        (void)hipFree(world_slot);
+        world_slot = nullptr;
         (void)hipFree(shapes);
         (void)hipFree(materials);
         (void)hipFree(patterns);
@@ -80,10 +83,18 @@ struct rt_context {
     rtc::DeviceWorld<float> w32;
     rtc::DeviceWorld<double> w64;
     rtc::FlopScene flops;  // per-kind shape counts for the algorithmic FLOP model
-    bool persistent_direct = false;  // scheduling of each kernel (RTC_SCHED_DIRECT / RTC_SCHED_POOL)
-    bool persistent_pool = true;
-    size_t occ_lds[4] = {0, 0, 0, 0};  // occupancy cache: {direct,pool} x {f32,f64}
-    int occ_blocks[4] = {0, 0, 0, 0};
+    // Defaults from A/B on MI355X (scripts/ab_sched.sh, scripts/stamps2.sh):
+    // uniform-cost direct tiles -> static stride; high-variance pool tiles ->
+    // per-XCD atomic queues; per-lane stores beat LDS-staged ones (the
+    // staging barriers wait for store completion).
+    uint32_t sched_direct = rtc::kSchedStatic;  // RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic
+    uint32_t sched_pool = rtc::kSchedDynamic;
+    bool staged_store = false;  // RTC_STAGED_STORE=1 stages tile pixels in LDS
+    bool lds_world = true;      // RTC_LDS_WORLD=0 gathers shade data from global memory
+    size_t occ_lds[8] = {};     // occupancy cache: {direct,pool} x {f32,f64} x {global,LDS world}
+    int occ_blocks[8] = {};
+    unsigned long long* d_stamps = nullptr;  // RT_FLAG_STAMPS diagnostics
+    uint32_t stamp_capacity = 0, stamp_count = 0;
     void* d_scratch = nullptr;  // host-buffer renders / color_at staging
     size_t scratch_bytes = 0;
 };
@@ -133,6 +144,10 @@ int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes,
         }
     }
     begin[kNumKinds] = (int32_t)sh.size();
+    // world order -> (slot | kind << 24), padded to whole 16-byte words
+    std::vector<int32_t> ws((sh.size() + 3) / 4 * 4, -1);
+    for (int k = 0; k < kNumKinds; ++k)
+        for (int32_t j = begin[k]; j < begin[k + 1]; ++j) ws[sh[j].world_index] = j | (k << 24);
     std::vector<MaterialRec<R>> mt(nm);
     bool any_secondary = false;
     for (uint32_t i = 0; i < nm; ++i) {
@@ -171,13 +186,16 @@ int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes,
         }
     int rc;
     if ((rc = upload(&w.shapes, sh)) || (rc = upload(&w.materials, mt)) || (rc = upload(&w.patterns, pt)) ||
-        (rc = upload(&w.lights, lt)))
+        (rc = upload(&w.lights, lt)) || (rc = upload(&w.world_slot, ws)))
         return rc;
     w.scene.shapes = w.shapes;
     w.scene.materials = w.materials;
     w.scene.patterns = w.patterns;
     w.scene.lights = w.lights;
+    w.scene.world_slot = w.world_slot;
     for (int k = 0; k <= kNumKinds; ++k) w.scene.kind_begin[k] = begin[k];
+    w.scene.n_materials = (int32_t)nm;
+    w.scene.n_patterns = (int32_t)np;
     w.scene.n_lights = (int32_t)nl;
     w.scene.any_secondary = any_secondary ? 1 : 0;
     return RT_OK;
@@ -203,7 +221,7 @@ int validate_scene(const rt_shape_desc* shapes, uint32_t ns, const rt_material_d
             (pats[i].sub_a < 0 || pats[i].sub_b < 0 || (uint32_t)pats[i].sub_a >= np || (uint32_t)pats[i].sub_b >= np))
             return set_error(RT_ERR_INVALID, "pattern " + std::to_string(i) + ": bad sub-pattern index");
     }
-    if (ns > 0x7fffffff || nl > 0x7fffffff) return set_error(RT_ERR_INVALID, "table too large");
+    if (ns > 0xFFFFFF || nl > 0x7fffffff) return set_error(RT_ERR_INVALID, "table too large");
     return RT_OK;
 }
 
@@ -220,11 +238,12 @@ size_t pool_lds_bytes(uint32_t cap) {
     return 3 * kBlock * sizeof(long long) + (size_t)cap * (7 * sizeof(R) + sizeof(uint32_t));
 }
 
-constexpr size_t kMaxLds = 160 * 1024 - 1024;  // leave room for static LDS
+constexpr size_t kMaxLds = 160 * 1024 - 8 * 1024;  // leave room for static LDS (tile staging)
 
 struct LaunchShape {
     bool pool;
-    bool persistent;
+    uint32_t world_lds;  // world tables staged in LDS (bytes, 0 = none)
+    uint32_t sched;
     uint32_t grid;
     size_t lds;
     uint32_t cap, batch;
@@ -233,30 +252,35 @@ struct LaunchShape {
 template <typename R>
 int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t n_tiles, LaunchShape& ls) {
     ls.pool = sc.any_secondary && depth > 0;
-    ls.lds = 0;
+    const size_t wb = world_lds_bytes<R>(sc.kind_begin[kNumKinds], sc.n_materials, sc.n_patterns);
+    ls.world_lds = (ctx->lds_world && wb <= kMaxWorldLds) ? (uint32_t)wb : 0;
+    ls.lds = ls.world_lds;
     ls.cap = ls.batch = 0;
     if (ls.pool) {
+        const size_t room = kMaxLds - ls.world_lds;
         uint32_t batch = kBlock;
-        while (batch > 32 && pool_lds_bytes<R>(pool_capacity(depth, batch)) > kMaxLds) batch /= 2;
-        if (pool_lds_bytes<R>(pool_capacity(depth, batch)) > kMaxLds)
+        while (batch > 32 && pool_lds_bytes<R>(pool_capacity(depth, batch)) > room) batch /= 2;
+        if (pool_lds_bytes<R>(pool_capacity(depth, batch)) > room)
             return set_error(RT_ERR_INVALID, "max_depth too large for the LDS ray pool");
         ls.batch = batch;
         ls.cap = pool_capacity(depth, batch);
-        ls.lds = pool_lds_bytes<R>(ls.cap);
+        ls.lds += pool_lds_bytes<R>(ls.cap);
     }
-    const int key = (ls.pool ? 1 : 0) + (sizeof(R) == 8 ? 2 : 0);
+    const int key = (ls.pool ? 1 : 0) + (sizeof(R) == 8 ? 2 : 0) + (ls.world_lds ? 4 : 0);
     int per_cu = 0;
     if (ctx->occ_lds[key] == ls.lds && ctx->occ_blocks[key] > 0) {
         per_cu = ctx->occ_blocks[key];
     } else {
-        RT_HIP(occupancy<R>(ls.pool, ls.lds, &per_cu));
+        RT_HIP(occupancy<R>(ls.pool, ls.world_lds != 0, ls.lds, &per_cu));
         ctx->occ_lds[key] = ls.lds;
         ctx->occ_blocks[key] = per_cu;
     }
     if (per_cu < 1) per_cu = 1;
     const uint64_t resident = (uint64_t)per_cu * (uint64_t)ctx->cu_count;
-    ls.persistent = ls.pool ? ctx->persistent_pool : ctx->persistent_direct;
-    ls.grid = ls.persistent ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, resident)) : n_tiles;
+    // The direct kernel has no tile queue (its tiles cost the same): a
+    // dynamic request runs as the static persistent grid.
+    ls.sched = ls.pool ? ctx->sched_pool : (ctx->sched_direct == kSchedDynamic ? kSchedStatic : ctx->sched_direct);
+    ls.grid = ls.sched != kSchedGrid ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, resident)) : n_tiles;
     return RT_OK;
 }
 
@@ -296,14 +320,16 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     if (rc) return rc;
     P.pool_capacity = ls.cap;
     P.pop_batch = ls.batch;
-    P.persistent = ls.persistent ? 1 : 0;
+    P.persistent = ls.sched;
     P.dequeue_chunk = ls.pool ? kDequeueChunkPool : kDequeueChunkDirect;
+    P.staged_store = ctx->staged_store ? 1 : 0;
     P.flags = flags;
+    P.world_lds = ls.world_lds;
     // Queue q holds tiles q, q+8, ... and serves workgroups q, q+8, ....  The
     // atomics one launch makes on queue q: one per chunk handed out, plus one
     // failing fetch per workgroup — except the workgroup that ends inside a
     // partial last chunk, which stops without fetching again.
-    for (int q = 0; q < kTileQueues && ls.persistent; ++q) {
+    for (int q = 0; q < kTileQueues && ls.sched == kSchedDynamic; ++q) {
         P.tile_base[q] = ctx->tile_base[q];
         const uint64_t C = P.dequeue_chunk;
         const uint64_t tiles_q = P.n_tiles > (uint32_t)q ? (P.n_tiles - q + kTileQueues - 1) / kTileQueues : 0;
@@ -311,6 +337,17 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
         const uint64_t blocks_q = ls.grid > (uint32_t)q ? (ls.grid - q + kTileQueues - 1) / kTileQueues : 0;
         const uint64_t partial_q = (tiles_q % C) != 0 ? 1 : 0;
         ctx->tile_base[q] += chunks_q + blocks_q - partial_q;
+    }
+    if (flags & RT_FLAG_STAMPS) {
+        if (ctx->stamp_capacity < ls.grid) {
+            (void)hipFree(ctx->d_stamps);
+            ctx->d_stamps = nullptr;
+            ctx->stamp_capacity = 0;
+            RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_stamps), 2 * sizeof(unsigned long long) * ls.grid));
+            ctx->stamp_capacity = ls.grid;
+        }
+        P.stamps = ctx->d_stamps;
+        ctx->stamp_count = ls.grid;
     }
     RT_HIP(launch_trace<R>(P, ls.pool, ls.grid, ls.lds, stream));
     return RT_OK;
@@ -409,10 +446,20 @@ int rt_context_create(int device_ordinal, rt_context** out) {
     hipDeviceProp_t prop;
     RT_HIP(hipGetDeviceProperties(&prop, device_ordinal));
     ctx->cu_count = prop.multiProcessorCount;
-    // scheduling knobs: "persistent" (resident grid + per-XCD tile queues) or
-    // "grid" (one workgroup per tile, the hardware dispatcher balances)
-    if (const char* e = std::getenv("RTC_SCHED_DIRECT")) ctx->persistent_direct = std::strcmp(e, "persistent") == 0;
-    if (const char* e = std::getenv("RTC_SCHED_POOL")) ctx->persistent_pool = std::strcmp(e, "grid") != 0;
+    // scheduling knobs: "grid" (one workgroup per tile, the hardware dispatcher
+    // balances), "static" (resident grid, fixed tile stride) or "dynamic"
+    // (resident grid + per-XCD atomic tile queues)
+    auto sched = [](const char* e, uint32_t dflt) {
+        if (!e) return dflt;
+        if (!std::strcmp(e, "grid")) return kSchedGrid;
+        if (!std::strcmp(e, "static")) return kSchedStatic;
+        if (!std::strcmp(e, "dynamic") || !std::strcmp(e, "persistent")) return kSchedDynamic;
+        return dflt;
+    };
+    ctx->sched_direct = sched(std::getenv("RTC_SCHED_DIRECT"), ctx->sched_direct);
+    ctx->sched_pool = sched(std::getenv("RTC_SCHED_POOL"), ctx->sched_pool);
+    if (const char* e = std::getenv("RTC_STAGED_STORE")) ctx->staged_store = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("RTC_LDS_WORLD")) ctx->lds_world = std::strcmp(e, "0") != 0;
     RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreate(&ctx->ev_start));
     RT_HIP(hipEventCreate(&ctx->ev_stop));
@@ -437,6 +484,7 @@ int rt_context_destroy(rt_context* ctx) {
     (void)hipFree(ctx->d_counters);
     (void)hipFree(ctx->d_error);
     (void)hipFree(ctx->d_scratch);
+    (void)hipFree(ctx->d_stamps);
     if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
     if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -563,6 +611,17 @@ int rt_color_at(rt_context* ctx, const double* rays, uint64_t n, uint32_t depth,
         if ((rc = read_counters(ctx, after))) return rc;
         fill_stats(ctx, before, after, ms, stats);
     }
+    return RT_OK;
+}
+
+int rt_debug_stamps(rt_context* ctx, uint64_t* out, uint32_t max_wg, uint32_t* n) {
+    if (!ctx || !n) return set_error(RT_ERR_INVALID, "null argument");
+    RT_HIP(hipSetDevice(ctx->device));
+    RT_HIP(hipDeviceSynchronize());
+    *n = ctx->stamp_count;
+    const uint32_t copy = std::min(max_wg, ctx->stamp_count);
+    if (out && copy)
+        RT_HIP(hipMemcpy(out, ctx->d_stamps, 2 * sizeof(uint64_t) * copy, hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

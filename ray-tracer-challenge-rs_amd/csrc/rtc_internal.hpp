@@ -37,8 +37,15 @@ constexpr int kCounterShards = 256;
 // pulls from queue b % 8 (blocks b and b+8 share an XCD under round-robin
 // dispatch; placement only affects speed).
 constexpr int kTileQueues = 8;
+// Tile scheduling modes (RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic)
+constexpr uint32_t kSchedGrid = 0;     // one workgroup per tile; the dispatcher balances
+constexpr uint32_t kSchedDynamic = 1;  // resident grid, per-XCD atomic tile queues
+constexpr uint32_t kSchedStatic = 2;   // resident grid, tiles b, b+G, ... (no atomics)
 constexpr int kDequeueChunkDirect = 4;  // tiles per dequeue: cheap, uniform tiles
 constexpr int kDequeueChunkPool = 1;    // costly, high-variance tiles: balance first
+// World tables up to this size are staged into LDS for the per-lane gathers
+// (~120 f32 shapes); larger worlds gather from global memory (L2-resident).
+constexpr size_t kMaxWorldLds = 16 * 1024;
 
 // Fixed-point pixel accumulator of the pool kernel: contributions are summed
 // as int64 multiples of 2^-48 so the per-pixel sum is independent of the
@@ -77,6 +84,17 @@ struct alignas(16) PatternRec {
     int32_t pad;
 };
 
+// LDS image of the world: [shapes][materials][patterns][world_slot], every
+// record a multiple of 16 bytes so each section stays 16-byte aligned.
+template <typename R>
+constexpr size_t world_lds_bytes(size_t ns, size_t nm, size_t np) {
+    return ns * sizeof(ShapeRec<R>) + nm * sizeof(MaterialRec<R>) + np * sizeof(PatternRec<R>) +
+           (ns + 3) / 4 * 16;
+}
+static_assert(sizeof(ShapeRec<float>) % 16 == 0 && sizeof(ShapeRec<double>) % 16 == 0);
+static_assert(sizeof(MaterialRec<float>) % 16 == 0 && sizeof(MaterialRec<double>) % 16 == 0);
+static_assert(sizeof(PatternRec<float>) % 16 == 0 && sizeof(PatternRec<double>) % 16 == 0);
+
 template <typename R>
 struct alignas(16) LightRec {
     R position[3];
@@ -96,7 +114,16 @@ struct DevScene {
     const MaterialRec<R>* materials;
     const PatternRec<R>* patterns;
     const LightRec<R>* lights;
+    const int32_t* world_slot;  // world order -> slot | kind << 24 (rounded up to 4 entries)
+    // Per-lane gathers (the hit's shape, its material and pattern) go through
+    // these: LDS copies staged at kernel start when the tables fit
+    // (LaunchParams::world_lds), else the global tables above.
+    const ShapeRec<R>* lshapes;
+    const MaterialRec<R>* lmats;
+    const PatternRec<R>* lpats;
+    const int32_t* lworld_slot;
     int32_t kind_begin[kNumKinds + 1];
+    int32_t n_materials, n_patterns;
     int32_t n_lights;
     int32_t any_secondary;  // some material has reflectiveness or transparency != 0
 };
@@ -118,9 +145,12 @@ struct LaunchParams {
     uint32_t max_depth;      // `remaining` of the primary ray
     uint32_t pool_capacity;  // pool kernel: rays held in LDS
     uint32_t pop_batch;      // pool kernel: rays popped per iteration (<= kBlock)
-    uint32_t persistent;     // 1: resident grid dequeues tiles; 0: one workgroup per tile
+    uint32_t persistent;     // kSched*: tile scheduling of this launch
     uint32_t dequeue_chunk;  // tiles per dequeue (persistent mode)
+    uint32_t staged_store;   // stage tile pixels in LDS for contiguous stores
     uint32_t flags;          // RT_FLAG_* diagnostic ablations
+    uint32_t world_lds;      // bytes of world tables staged at the start of dynamic LDS (0 = none)
+    unsigned long long* stamps;  // RT_FLAG_STAMPS: 2 x grid s_memrealtime values
     unsigned long long* tile_counter;  // kTileQueues cumulative dequeue counters (one per XCD)
     unsigned long long tile_base[kTileQueues];  // their values at this launch's start
     unsigned long long* counters;      // kCounterShards x kNumCounters cumulative u64

@@ -192,25 +192,47 @@ __device__ inline bool odd_i64(R v) {
 }
 
 // -------------------------------------------------------- shape intersect
-// Each routine calls emit(t) once per entry, in the reference's push order.
+// Each routine calls emit(t, valid) once per POTENTIAL entry, in the
+// reference's push order; `valid` says whether the reference pushes it.
+// Masks replace the reference's early returns so a wave never splits around
+// a shape test: a divergent branch costs exec-mask SALU work and stalls
+// (MI355X PMC: ~350 SALU per pixel-wave with branches), a select one VALU op.
+// Masked-out lanes may compute inf/NaN; they are never emitted as valid.
 
-// utils.rs:47-57
+// utils.rs:47-57; `ok` masks the caller's own guard
 template <typename R, typename F>
-__device__ inline void quadratic(R a, R b, R c, F&& emit2) {
+__device__ inline void quadratic(R a, R b, R c, bool ok, F&& emit2) {
     const R disc = Real<R>::rfma((R)4 * a, -c, b * b);
-    if (disc < (R)0) return;
+    const bool v = ok && !(disc < (R)0);
     const R da = (R)2 * a;
     const R root = Real<R>::sqrt(disc);
     if constexpr (sizeof(R) == 4) {
         const R ri = __builtin_amdgcn_rcpf(da);
-        emit2((-b - root) * ri, (-b + root) * ri);
+        emit2((-b - root) * ri, (-b + root) * ri, v);
     } else {
-        emit2((-b - root) / da, (-b + root) / da);
+        emit2((-b - root) / da, (-b + root) / da, v);
     }
 }
 
-template <typename R, int K, typename F>
+template <typename R>
+__device__ inline R sel(bool c, R a, R b) {
+    return c ? a : b;
+}
+
+// kNearest: the caller only wants the nearest t >= 0 of this shape (the
+// closest-hit loop).  For a sphere or cube the two entries satisfy t1 <= t2
+// with one validity, so t2 can only be that t when t1 < 0: emit one
+// candidate instead of two (same result, half the hit bookkeeping).
+template <typename R, int K, bool kNearest = false, typename F>
 __device__ inline void entries(const ShapeRec<R>& s, V3<R> o, V3<R> d, F&& emit) {
+    auto emit_pair = [&](R t1, R t2, bool v) {
+        if constexpr (kNearest) {
+            emit(sel(t1 >= (R)0, t1, t2), v);
+        } else {
+            emit(t1, v);
+            emit(t2, v);
+        }
+    };
     using T = Real<R>;
     if constexpr (K == RT_SHAPE_SPHERE) {  // sphere.rs:41-53
         const R a = dot(d, d);
@@ -222,42 +244,32 @@ __device__ inline void entries(const ShapeRec<R>& s, V3<R> o, V3<R> d, F&& emit)
             // shadow_puppets.yaml, a sphere scaled by 0.01 in z).
             const V3<R> c = cross(d, o);
             const R disc = (R)4 * (a - dot(c, c));
-            if (disc < (R)0) return;
+            const bool v = !(disc < (R)0);
             const R root = T::sqrt(disc);
             const R ri = __builtin_amdgcn_rcpf((R)2 * a);
-            emit((-b - root) * ri);
-            emit((-b + root) * ri);
+            emit_pair((-b - root) * ri, (-b + root) * ri, v);
         } else {
             const R c = dot(o, o) - (R)1;
-            quadratic<R>(a, b, c, [&](R t1, R t2) {
-                emit(t1);
-                emit(t2);
-            });
+            quadratic<R>(a, b, c, true, emit_pair);
         }
     } else if constexpr (K == RT_SHAPE_PLANE) {  // plane.rs:42-48
-        if (T::fabs(d.y) < T::kEps) return;
-        emit(T::div(-o.y, d.y));
+        emit(T::div(-o.y, d.y), !(T::fabs(d.y) < T::kEps));
     } else if constexpr (K == RT_SHAPE_CUBE) {  // cube.rs:22-43, 65-85
         auto axis = [&](R org, R dir, R& lo, R& hi) {
             const R nmin = (R)-1 - org, nmax = (R)1 - org;
-            if (T::fabs(dir) >= T::kEps) {
-                if constexpr (sizeof(R) == 4) {
-                    const R r = __builtin_amdgcn_rcpf(dir);
-                    lo = nmin * r;
-                    hi = nmax * r;
-                } else {
-                    lo = nmin / dir;
-                    hi = nmax / dir;
-                }
+            const bool steep = T::fabs(dir) >= T::kEps;
+            R l, h;
+            if constexpr (sizeof(R) == 4) {
+                const R r = sel(steep, __builtin_amdgcn_rcpf(dir), T::kMax);
+                l = nmin * r;
+                h = nmax * r;
             } else {
-                lo = nmin * T::kMax;
-                hi = nmax * T::kMax;
+                l = sel(steep, nmin / dir, nmin * T::kMax);
+                h = sel(steep, nmax / dir, nmax * T::kMax);
             }
-            if (lo > hi) {
-                const R tmp = lo;
-                lo = hi;
-                hi = tmp;
-            }
+            const bool swap = l > h;
+            lo = sel(swap, h, l);
+            hi = sel(swap, l, h);
         };
         R xn, xx, yn, yx, zn, zx;
         axis(o.x, d.x, xn, xx);
@@ -265,68 +277,58 @@ __device__ inline void entries(const ShapeRec<R>& s, V3<R> o, V3<R> d, F&& emit)
         axis(o.z, d.z, zn, zx);
         const R tmin = T::fmax(T::fmax(T::fmax(-T::kMax, xn), yn), zn);
         const R tmax = T::fmin(T::fmin(T::fmin(T::kMax, xx), yx), zx);
-        if (tmin < tmax && tmax > (R)0) {
-            emit(tmin);
-            emit(tmax);
-        }
+        emit_pair(tmin, tmax, (tmin < tmax) & (tmax > (R)0));
     } else if constexpr (K == RT_SHAPE_CYLINDER || K == RT_SHAPE_CONE) {
         const R ymin = s.ymin, ymax = s.ymax;
-        auto side = [&](R t1, R t2) {
-            if (t1 > t2) {
-                const R tmp = t1;
-                t1 = t2;
-                t2 = tmp;
-            }
+        auto side = [&](R t1, R t2, bool v) {
+            const bool swap = t1 > t2;
+            const R lo = sel(swap, t2, t1), hi = sel(swap, t1, t2);
             R y1, y2;
             if constexpr (K == RT_SHAPE_CYLINDER) {  // cylinder.rs:96-104
-                y1 = T::rfma(t1, d.y, o.y);
-                y2 = T::rfma(t2, d.y, o.y);
+                y1 = T::rfma(lo, d.y, o.y);
+                y2 = T::rfma(hi, d.y, o.y);
             } else {  // cone.rs:99-107
-                y1 = T::rfma(d.y, t1, o.y);
-                y2 = T::rfma(d.y, t2, o.y);
+                y1 = T::rfma(d.y, lo, o.y);
+                y2 = T::rfma(d.y, hi, o.y);
             }
-            if (ymin < y1 && y1 < ymax) emit(t1);
-            if (ymin < y2 && y2 < ymax) emit(t2);
+            emit(lo, v && ymin < y1 && y1 < ymax);
+            emit(hi, v && ymin < y2 && y2 < ymax);
         };
         if constexpr (K == RT_SHAPE_CYLINDER) {  // cylinder.rs:81-110
             const R a = d.x * d.x + d.z * d.z;
-            if (T::fabs(a) > (R)0) {
-                const R b = (R)2 * T::rfma(o.x, d.x, o.z * d.z);
-                const R c = o.x * o.x + o.z * o.z - (R)1;
-                quadratic<R>(a, b, c, side);
-            }
+            const R b = (R)2 * T::rfma(o.x, d.x, o.z * d.z);
+            const R c = o.x * o.x + o.z * o.z - (R)1;
+            quadratic<R>(a, b, c, T::fabs(a) > (R)0, side);
         } else {  // cone.rs:81-112
             const R a = d.x * d.x - d.y * d.y + d.z * d.z;
             const R b = (R)2 * T::rfma(o.z, d.z, T::rfma(o.x, d.x, -o.y * d.y));
             const R c = o.x * o.x - o.y * o.y + o.z * o.z;
-            if (T::fabs(a) < T::kEps && T::fabs(b) > T::kEps)
-                emit(T::div(-c, (R)2 * b));
-            else
-                quadratic<R>(a, b, c, side);
+            const bool single = T::fabs(a) < T::kEps && T::fabs(b) > T::kEps;
+            emit(T::div(-c, (R)2 * b), single);
+            quadratic<R>(a, b, c, !single, side);
         }
         // intersect_caps: cylinder.rs:41-58 / cone.rs:41-58
-        if (!s.closed || T::fabs(d.y) < T::kEps) return;
+        const bool caps = s.closed && !(T::fabs(d.y) < T::kEps);
         const R r_lo = (K == RT_SHAPE_CYLINDER) ? (R)1 : ymin * ymin;
         const R r_hi = (K == RT_SHAPE_CYLINDER) ? (R)1 : ymax * ymax;
         R t = T::div(ymin - o.y, d.y);
         R x = T::rfma(d.x, t, o.x), z = T::rfma(d.z, t, o.z);
-        if (x * x + z * z <= r_lo) emit(t);
+        emit(t, caps && x * x + z * z <= r_lo);
         t = T::div(ymax - o.y, d.y);
         x = T::rfma(d.x, t, o.x);
         z = T::rfma(d.z, t, o.z);
-        if (x * x + z * z <= r_hi) emit(t);
+        emit(t, caps && x * x + z * z <= r_hi);
     } else {  // triangle.rs:39-56
         const V3<R> e1 = {s.tri[3], s.tri[4], s.tri[5]};
         const V3<R> e2 = {s.tri[6], s.tri[7], s.tri[8]};
         const V3<R> dce2 = cross(d, e2);
         const R det = dot(e1, dce2);
-        if (T::fabs(det) < T::kEps) return;
         const V3<R> v1o = vsub(o, V3<R>{s.tri[0], s.tri[1], s.tri[2]});
         const R u = T::div(dot(v1o, dce2), det);
-        if (!(u >= (R)0 && u <= (R)1)) return;
         const V3<R> oce1 = cross(v1o, e1);
         const R v = T::div(dot(d, oce1), det);
-        if (v > (R)0 && u + v < (R)1) emit(T::div(dot(e2, oce1), det));
+        emit(T::div(dot(e2, oce1), det),
+             !(T::fabs(det) < T::kEps) && (u >= (R)0 && u <= (R)1) && v > (R)0 && u + v < (R)1);
     }
 }
 
@@ -366,31 +368,35 @@ struct Hit {
     R t;
     int slot;   // index into the kind-sorted shape table, -1 = miss
     int world;  // world order, for the stable-sort tie rule
-    int entry;  // push order within the shape
     int kind;
 };
 
 // collect_intersections + hit (world.rs:25-35, intersections.rs:13-18):
-// the first minimum t >= 0 in (t, world order, push order).
+// the first minimum t >= 0 in (t, world order, push order).  Within one
+// shape a later entry never displaces an equal t (strict `w < world`), so
+// push order needs no tracking; the loop carries (t, world) only and the
+// slot/kind come from the world_slot table afterwards.
 template <typename R>
 __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
-    Hit<R> h{Real<R>::kInf, -1, INT_MAX, 0, -1};
-    for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
+    R ht = Real<R>::kInf;
+    int hw = INT_MAX;
+    for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int) {
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
         const int w = s.world_index;
-        int e = 0;
-        entries<R, K>(s, lo, ld, [&](R t) {
-            if (t >= (R)0 && (t < h.t || (t == h.t && w < h.world))) {
-                h.t = t;
-                h.slot = slot;
-                h.world = w;
-                h.entry = e;
-                h.kind = K;
-            }
-            ++e;
+        entries<R, K, true>(s, lo, ld, [&](R t, bool v) {
+            // bitwise, not short-circuit: && / || would be lowered to divergent branches
+            const bool better = v & (t >= (R)0) & ((t < ht) | ((t == ht) & (w < hw)));
+            ht = sel(better, t, ht);
+            hw = better ? w : hw;
         });
     });
+    Hit<R> h{ht, -1, hw, -1};
+    if (hw != INT_MAX) {
+        const uint32_t ws = (uint32_t)sc.lworld_slot[hw];
+        h.slot = (int)(ws & 0xFFFFFFu);
+        h.kind = (int)(ws >> 24);
+    }
     return h;
 }
 
@@ -399,10 +405,10 @@ template <typename R>
 __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) {
     bool hit = false;
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int) {
-        if (!s.casts_shadow) return;
+        if (!s.casts_shadow) return;  // wave-uniform
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
-        entries<R, K>(s, lo, ld, [&](R t) { hit = hit || (t >= (R)0 && t < dist); });
+        entries<R, K>(s, lo, ld, [&](R t, bool v) { hit |= v & (t >= (R)0) & (t < dist); });
     });
     return hit;
 }
@@ -421,7 +427,9 @@ __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> 
     auto before = [](const Key& a, const Key& b) {
         return a.t < b.t || (a.t == b.t && (a.w < b.w || (a.w == b.w && a.e < b.e)));
     };
-    const Key hk{h.t, h.world, h.entry};
+    // The hit's own entry is the first of its shape at t == h.t, so entries
+    // of that shape sort before it iff t < h.t: push order 0 says exactly that.
+    const Key hk{h.t, h.world, 0};
     bool have_all = false, have_other = false, hit_present = false;
     Key best_all{}, best_other{};
     int mat_all = -1, mat_other = -1;
@@ -431,13 +439,13 @@ __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> 
         const int w = s.world_index;
         int e = 0, count = 0;
         Key last{};
-        entries<R, K>(s, lo, ld, [&](R t) {
+        entries<R, K>(s, lo, ld, [&](R t, bool v) {
             const Key k{t, w, e};
-            if (before(k, hk)) {
+            if (v && before(k, hk)) {
                 ++count;
                 if (count == 1 || before(last, k)) last = k;
             }
-            ++e;
+            e += v ? 1 : 0;
         });
         if (count & 1) {
             if (!have_all || before(best_all, last)) {
@@ -454,11 +462,11 @@ __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> 
             }
         }
     });
-    n1 = have_all ? sc.materials[mat_all].refractive_index : (R)1;
+    n1 = have_all ? sc.lmats[mat_all].refractive_index : (R)1;
     if (hit_present)  // the hit removes itself from the list
-        n2 = have_other ? sc.materials[mat_other].refractive_index : (R)1;
+        n2 = have_other ? sc.lmats[mat_other].refractive_index : (R)1;
     else              // the hit pushes itself
-        n2 = sc.materials[sc.shapes[h.slot].material].refractive_index;
+        n2 = sc.lmats[sc.lshapes[h.slot].material].refractive_index;
 }
 
 // shape.rs:22-27 + local_normal_at of each shape
@@ -506,7 +514,7 @@ __device__ inline V3<R> normal_at(const ShapeRec<R>& s, int kind, V3<R> p) {
 template <typename R>
 __device__ inline V3<R> pattern_color(const DevScene<R>& sc, int pid, const ShapeRec<R>& s, V3<R> p) {
     using T = Real<R>;
-    const PatternRec<R>* pr = &sc.patterns[pid];
+    const PatternRec<R>* pr = &sc.lpats[pid];
     const V3<R> pp = xform_point(pr->inv, xform_point(s.inv, p));
     for (int guard = 0; guard < 16; ++guard) {
         switch (pr->kind) {
@@ -531,7 +539,7 @@ __device__ inline V3<R> pattern_color(const DevScene<R>& sc, int pid, const Shap
                                     : v3(pr->color_a[0], pr->color_a[1], pr->color_a[2]);
             }
             case RT_PATTERN_COMPLEX:  // complex_pattern.rs:25-32: sub transforms ignored
-                pr = &sc.patterns[odd_i64(T::floor(pp.x)) ? pr->sub_b : pr->sub_a];
+                pr = &sc.lpats[odd_i64(T::floor(pp.x)) ? pr->sub_b : pr->sub_a];
                 continue;
             default:  // TestPattern (pattern.rs:55-58)
                 return pp;
@@ -562,13 +570,13 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
     const Hit<R> h = closest_hit(sc, o, d);
     if (h.slot < 0) return false;  // world.rs:85: miss -> BLACK
     k.c[4]++;                      // shaded
-    const ShapeRec<R>& s = sc.shapes[h.slot];
+    const ShapeRec<R>& s = sc.lshapes[h.slot];
     // prepare_computations, intersection.rs:21-31
     const V3<R> p = along(o, d, h.t);
     V3<R> n = normal_at(s, h.kind, p);
     const V3<R> eye = vneg(d);
     if (dot(n, eye) < (R)0) n = vneg(n);
-    const MaterialRec<R>& m = sc.materials[s.material];
+    const MaterialRec<R>& m = sc.lmats[s.material];
     const V3<R> over = along(p, n, T::kOffset);  // computed_hit.rs:33
     // material.rs:75-80: the pattern is sampled at over_point, once per hit
     V3<R> base = {m.color[0], m.color[1], m.color[2]};
@@ -730,19 +738,39 @@ __device__ inline void load_primary(const LaunchParams<R>& P, uint32_t t, uint32
     }
 }
 
+// Wave reduction of the event counters, then lane 0 adds them into the wave's
+// counter shard (no LDS, no barrier).
 __device__ inline void flush_counts(const Counts& k, unsigned long long* global) {
-    __shared__ unsigned long long s_counts[kNumCounters];
-    if (threadIdx.x < kNumCounters) s_counts[threadIdx.x] = 0;
-    __syncthreads();
+    const uint32_t shard = (blockIdx.x * (kBlock / 64) + threadIdx.x / 64) % kCounterShards;
     for (int i = 0; i < kNumCounters; ++i) {
-        // wave reduction, then one LDS atomic per wave
-        unsigned long long v = k.c[i];
+        unsigned int v = k.c[i];
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&s_counts[i], v);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&global[shard * kNumCounters + i], (unsigned long long)v);
     }
+}
+
+// Write one tile of RT_OUT_REAL pixels: colours are staged in LDS in the
+// output's row-major order and written back one element per lane, so each
+// wave-wide store covers 64 consecutive elements (256 B for f32) instead of
+// three 12-byte-strided partial lines per pixel.  Canvas edges are masked.
+template <typename R>
+__device__ inline void store_tile(const LaunchParams<R>& P, uint32_t t, V3<R> c, R* s_px) {
+    const uint32_t tid = threadIdx.x;
+    s_px[3 * tid + 0] = c.x;
+    s_px[3 * tid + 1] = c.y;
+    s_px[3 * tid + 2] = c.z;
     __syncthreads();
-    if (threadIdx.x < kNumCounters && s_counts[threadIdx.x])
-        atomicAdd(&global[(blockIdx.x % kCounterShards) * kNumCounters + threadIdx.x], s_counts[threadIdx.x]);
+    const uint32_t lrow = t / P.tiles_x, tcol = t - lrow * P.tiles_x;
+    const uint32_t x0 = tcol * RT_TILE_W, y0 = (lrow * P.shard_count + P.shard_index) * RT_TILE_H;
+    const uint32_t ncols = min((uint32_t)RT_TILE_W, P.width - x0);
+    const uint32_t nrows = y0 < P.height ? min((uint32_t)RT_TILE_H, P.height - y0) : 0u;
+    constexpr uint32_t kRowElems = 3 * RT_TILE_W;
+    R* out = static_cast<R*>(P.out) + ((uint64_t)lrow * RT_TILE_H * P.width + x0) * 3;
+    for (uint32_t i = tid; i < RT_TILE_H * kRowElems; i += kBlock) {
+        const uint32_t row = i / kRowElems, e = i - row * kRowElems;
+        if (row < nrows && e < 3 * ncols) out[(uint64_t)row * P.width * 3 + e] = s_px[i];
+    }
+    __syncthreads();  // s_px is reused by the next tile
 }
 
 // Next tile of this workgroup (called by thread 0 only; `chunk`/`pos` live in
@@ -752,7 +780,11 @@ __device__ inline void flush_counts(const Counts& k, unsigned long long* global)
 template <typename R>
 __device__ inline unsigned int next_tile(const LaunchParams<R>& P, uint32_t it, unsigned long long& chunk,
                                          uint32_t& pos) {
-    if (!P.persistent) return it == 0 ? blockIdx.x : 0xFFFFFFFFu;  // grid = one workgroup per tile
+    if (P.persistent == kSchedGrid) return it == 0 ? blockIdx.x : 0xFFFFFFFFu;  // one workgroup per tile
+    if (P.persistent == kSchedStatic) {  // resident grid, tiles b, b+G, b+2G, ... (no atomics)
+        const unsigned long long t = blockIdx.x + (unsigned long long)it * gridDim.x;
+        return t < P.n_tiles ? (unsigned int)t : 0xFFFFFFFFu;
+    }
     const uint32_t q = blockIdx.x % kTileQueues;
     if (it == 0 || pos == P.dequeue_chunk) {
         chunk = atomicAdd(&P.tile_counter[q], 1ull) - P.tile_base[q];
@@ -763,16 +795,47 @@ __device__ inline unsigned int next_tile(const LaunchParams<R>& P, uint32_t it, 
 }
 
 // The world as seen by one launch, rebuilt from the restrict parameters.
-template <typename R>
+// With kLds the shape/material/pattern tables are first copied into the
+// front of dynamic LDS (P.world_lds bytes, 16-byte words, one barrier) so
+// the per-lane gathers of shade_ray are ds_reads rather than divergent
+// global loads; the wave-uniform loops keep reading the global tables
+// through the scalar cache.
+template <typename R, bool kLds>
 __device__ inline DevScene<R> scene_view(const LaunchParams<R>& P, const ShapeRec<R>* __restrict__ shapes,
                                          const MaterialRec<R>* __restrict__ materials,
                                          const PatternRec<R>* __restrict__ patterns,
-                                         const LightRec<R>* __restrict__ lights) {
+                                         const LightRec<R>* __restrict__ lights, unsigned char* smem) {
     DevScene<R> sc = P.scene;
     sc.shapes = shapes;
     sc.materials = materials;
     sc.patterns = patterns;
     sc.lights = lights;
+    if constexpr (kLds) {
+        const int ns = sc.kind_begin[kNumKinds];
+        auto* ls = reinterpret_cast<ShapeRec<R>*>(smem);
+        auto* lm = reinterpret_cast<MaterialRec<R>*>(ls + ns);
+        auto* lp = reinterpret_cast<PatternRec<R>*>(lm + sc.n_materials);
+        auto* lw = reinterpret_cast<int32_t*>(lp + sc.n_patterns);
+        auto copy = [](void* dst, const void* src, uint32_t bytes) {
+            const uint4* s4 = static_cast<const uint4*>(src);
+            uint4* d4 = static_cast<uint4*>(dst);
+            for (uint32_t i = threadIdx.x; i < bytes / 16; i += kBlock) d4[i] = s4[i];
+        };
+        copy(ls, shapes, ns * (uint32_t)sizeof(ShapeRec<R>));
+        copy(lm, materials, sc.n_materials * (uint32_t)sizeof(MaterialRec<R>));
+        copy(lp, patterns, sc.n_patterns * (uint32_t)sizeof(PatternRec<R>));
+        copy(lw, sc.world_slot, (ns + 3) / 4 * 16);
+        __syncthreads();
+        sc.lworld_slot = lw;
+        sc.lshapes = ls;
+        sc.lmats = lm;
+        sc.lpats = lp;
+    } else {
+        sc.lshapes = shapes;
+        sc.lmats = materials;
+        sc.lpats = patterns;
+        sc.lworld_slot = sc.world_slot;
+    }
     return sc;
 }
 
@@ -781,40 +844,50 @@ __device__ inline DevScene<R> scene_view(const LaunchParams<R>& P, const ShapeRe
         const PatternRec<R>* __restrict__ patterns, const LightRec<R>* __restrict__ lights
 
 // --------------------------------------------------------------- kernels
-template <typename R>
+template <typename R, bool kLds>
 __global__ __launch_bounds__(kBlock) void trace_direct(LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
-    const DevScene<R> sc = scene_view(P, shapes, materials, patterns, lights);
-    __shared__ unsigned int s_tile[2];
+    extern __shared__ __align__(16) unsigned char smem[];
+    const DevScene<R> sc = scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem);
+    if (P.stamps && threadIdx.x == 0) P.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    __shared__ R s_px[3 * kBlock];
     Counts k = {};
     const uint32_t tid = threadIdx.x;
-    unsigned long long chunk = 0;
-    uint32_t pos = 0;
-    for (uint32_t it = 0;; ++it) {
-        if (tid == 0) s_tile[it & 1] = next_tile(P, it, chunk, pos);
-        __syncthreads();
-        const uint32_t t = s_tile[it & 1];
+    const bool staged = P.staged_store && !P.rays && P.out_format == RT_OUT_REAL;
+    // Tiles b, b+G, b+2G, ...: with G = n_tiles (kSchedGrid) one tile per
+    // workgroup, with G = resident workgroups (kSchedStatic) a persistent
+    // grid.  Primary-only tiles cost the same, so no queue is needed, and the
+    // tile index is an SGPR by construction (loop control stays scalar).
+    for (uint32_t t = blockIdx.x;; t += gridDim.x) {
         if (t >= P.n_tiles) break;
         bool valid;
         V3<R> o, d;
         uint64_t out_idx;
         load_primary(P, t, tid, valid, o, d, out_idx);
-        if (!valid) continue;
-        k.c[0]++;
-        Shaded<R> sh;
         V3<R> c = {(R)0, (R)0, (R)0};
-        if (P.flags & (RT_FLAG_NO_SHADE | RT_FLAG_NO_TRACE)) {
-            if (P.flags & RT_FLAG_NO_TRACE) {
-                c = d;
-            } else {
-                const Hit<R> h = closest_hit(sc, o, d);
-                c = {h.t * (R)0.01, (R)h.slot, (R)0};
+        if (valid) {
+            k.c[0]++;
+            Shaded<R> sh;
+            if (P.flags & (RT_FLAG_NO_SHADE | RT_FLAG_NO_TRACE)) {
+                if (P.flags & RT_FLAG_NO_TRACE) {
+                    c = d;
+                } else {
+                    const Hit<R> h = closest_hit(sc, o, d);
+                    c = {h.t * (R)0.01, (R)h.slot, (R)0};
+                }
+            } else if (shade_ray<R, false>(sc, o, d, 0, sh, k)) {
+                c = sh.surface;
             }
-        } else if (shade_ray<R, false>(sc, o, d, 0, sh, k)) {
-            c = sh.surface;
         }
-        store_pixel(P, out_idx, c);
+        if (staged)
+            store_tile(P, t, c, s_px);
+        else if (valid)
+            store_pixel(P, out_idx, c);
     }
     if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
+    if (P.stamps) {
+        __syncthreads();
+        if (threadIdx.x == 0) P.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 // Ray pool layout in dynamic LDS: [acc: 3 x kBlock i64][ox oy oz dx dy dz w : cap x R][meta : cap x u32]
@@ -855,12 +928,15 @@ __device__ inline void acc_add(long long* acc, uint32_t pix, double v) {
     if (q) atomicAdd(reinterpret_cast<unsigned long long*>(&acc[pix]), (unsigned long long)q);
 }
 
-template <typename R>
+template <typename R, bool kLds>
 __global__ __launch_bounds__(kBlock) void trace_pool(LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
-    const DevScene<R> sc = scene_view(P, shapes, materials, patterns, lights);
-    extern __shared__ __align__(16) unsigned char smem[];
+    extern __shared__ __align__(16) unsigned char smem_all[];
+    const DevScene<R> sc = scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem_all);
+    if (P.stamps && threadIdx.x == 0) P.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    unsigned char* smem = smem_all + (kLds ? P.world_lds : 0);
     __shared__ unsigned int s_tile[2];
     __shared__ int s_top[2];
+    __shared__ R s_px[3 * kBlock];
     const uint32_t cap = P.pool_capacity;
     Pool<R> pl;
     pl.acc = reinterpret_cast<long long*>(smem);
@@ -885,7 +961,7 @@ __global__ __launch_bounds__(kBlock) void trace_pool(LaunchParams<R> P, RTC_WORL
         }
         for (int c = 0; c < 3; ++c) pl.acc[c * kBlock + tid] = 0;
         __syncthreads();
-        const uint32_t t = s_tile[it & 1];
+        const uint32_t t = __builtin_amdgcn_readfirstlane(s_tile[it & 1]);
         if (t >= P.n_tiles) break;
         bool valid;
         V3<R> o, d;
@@ -944,15 +1020,19 @@ __global__ __launch_bounds__(kBlock) void trace_pool(LaunchParams<R> P, RTC_WORL
                 __syncthreads();
             }
         }
-        if (valid) {
-            const V3<R> c = {(R)((double)pl.acc[tid] * kAccInvScale),
-                             (R)((double)pl.acc[kBlock + tid] * kAccInvScale),
-                             (R)((double)pl.acc[2 * kBlock + tid] * kAccInvScale)};
+        const V3<R> c = {(R)((double)pl.acc[tid] * kAccInvScale), (R)((double)pl.acc[kBlock + tid] * kAccInvScale),
+                         (R)((double)pl.acc[2 * kBlock + tid] * kAccInvScale)};
+        if (P.staged_store && !P.rays && P.out_format == RT_OUT_REAL)
+            store_tile(P, t, c, s_px);
+        else if (valid)
             store_pixel(P, out_idx, c);
-        }
         __syncthreads();  // accumulators are re-zeroed for the next tile
     }
     if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
+    if (P.stamps) {
+        __syncthreads();
+        if (threadIdx.x == 0) P.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 // De-interleave gathered shard strips into one image.
@@ -974,27 +1054,34 @@ __global__ void assemble_shards(const unsigned char* __restrict__ gathered, unsi
 // ------------------------------------------------------------ launchers
 template <typename R>
 hipError_t launch_trace(const LaunchParams<R>& P, bool pool, uint32_t grid, size_t dyn_lds, hipStream_t stream) {
+    const bool lds = P.world_lds != 0;
+#define RTC_LAUNCH(K, L)                                                                                  \
+    hipLaunchKernelGGL((K<R, L>), dim3(grid), dim3(kBlock), dyn_lds, stream, P, P.scene.shapes, P.scene.materials, \
+                       P.scene.patterns, P.scene.lights)
     if (pool) {
-        hipLaunchKernelGGL(trace_pool<R>, dim3(grid), dim3(kBlock), dyn_lds, stream, P, P.scene.shapes,
-                           P.scene.materials, P.scene.patterns, P.scene.lights);
+        if (lds) RTC_LAUNCH(trace_pool, true);
+        else RTC_LAUNCH(trace_pool, false);
     } else {
-        hipLaunchKernelGGL(trace_direct<R>, dim3(grid), dim3(kBlock), 0, stream, P, P.scene.shapes,
-                           P.scene.materials, P.scene.patterns, P.scene.lights);
+        if (lds) RTC_LAUNCH(trace_direct, true);
+        else RTC_LAUNCH(trace_direct, false);
     }
+#undef RTC_LAUNCH
     return hipGetLastError();
 }
 
 template <typename R>
-hipError_t occupancy(bool pool, size_t dyn_lds, int* blocks_per_cu) {
+hipError_t occupancy(bool pool, bool lds, size_t dyn_lds, int* blocks_per_cu) {
     if (pool)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_pool<R>, kBlock, dyn_lds);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_direct<R>, kBlock, 0);
+        return lds ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_pool<R, true>, kBlock, dyn_lds)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_pool<R, false>, kBlock, dyn_lds);
+    return lds ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_direct<R, true>, kBlock, dyn_lds)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_direct<R, false>, kBlock, dyn_lds);
 }
 
 template hipError_t launch_trace<float>(const LaunchParams<float>&, bool, uint32_t, size_t, hipStream_t);
 template hipError_t launch_trace<double>(const LaunchParams<double>&, bool, uint32_t, size_t, hipStream_t);
-template hipError_t occupancy<float>(bool, size_t, int*);
-template hipError_t occupancy<double>(bool, size_t, int*);
+template hipError_t occupancy<float>(bool, bool, size_t, int*);
+template hipError_t occupancy<double>(bool, bool, size_t, int*);
 
 hipError_t launch_assemble(const void* gathered, void* image, uint32_t width, uint32_t height, uint32_t shards,
                            uint32_t strip_rows, uint32_t bpp, hipStream_t stream) {

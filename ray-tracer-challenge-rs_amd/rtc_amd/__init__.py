@@ -30,8 +30,8 @@ __all__ = [
     "RT_DEFAULT_MAX_DEPTH", "RT_TILE_H", "RT_TILE_W",
 ]
 
-RT_TILE_W = 16
-RT_TILE_H = 16
+RT_TILE_W = 64
+RT_TILE_H = 4
 RT_DEFAULT_MAX_DEPTH = 6  # World::MAX_REFLECTION_ITERATIONS, world.rs:15
 RT_MAX_SUPPORTED_DEPTH = 16
 
@@ -125,6 +125,10 @@ def _load() -> C.CDLL:
     # (libamdhip64.so.7) as /opt/rocm's.  Load it first so librtc binds to the
     # SAME runtime: torch streams, events and allocations are then valid
     # handles for the C-ABI (one HIP runtime per process).
+    # Kernel arguments in device memory: each wave's first s_load of its
+    # arguments then hits HBM/L2 instead of crossing PCIe (measured ~2 us per
+    # 1080p frame on MI355X).  Must be set before the HIP runtime starts.
+    os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
     try:
         import torch  # noqa: F401
     except ImportError:
@@ -148,6 +152,7 @@ def _load() -> C.CDLL:
         "rt_color_at": (C.c_int, [C.c_void_p, P(C.c_double), C.c_uint64, C.c_uint32, C.c_uint32, P(C.c_double),
                                   P(Stats)]),
         "rt_read_counters": (C.c_int, [C.c_void_p, P(Stats)]),
+        "rt_debug_stamps": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_uint32, P(C.c_uint32)]),
         "rt_assemble_shards": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                          C.c_void_p, C.c_void_p]),
         "rt_scene_load_yaml": (C.c_int, [C.c_char_p, P(C.c_void_p)]),
@@ -172,6 +177,7 @@ _lib = _load()
 EXPORTED_SYMBOLS = (
     "rt_abi_version", "rt_last_error", "rt_device_count", "rt_context_create", "rt_context_destroy",
     "rt_scene_upload", "rt_shard_rows", "rt_render", "rt_render_device", "rt_color_at", "rt_read_counters",
+    "rt_debug_stamps",
     "rt_assemble_shards", "rt_scene_load_yaml", "rt_scene_load_yaml_text", "rt_scene_view_get", "rt_scene_free",
     "rt_camera_make", "rt_camera_resize", "rt_matrix_inverse",
 )
@@ -340,6 +346,14 @@ class Context:
         _check(_lib.rt_color_at(self._h, r.ctypes.data_as(C.POINTER(C.c_double)), r.shape[0], depth,
                                 PRECISIONS[precision], out.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st)))
         return out, st.as_dict()
+
+    def debug_stamps(self) -> np.ndarray:
+        """(workgroups, 2) s_memrealtime {start, end} of the last RT_FLAG_STAMPS launch (100 MHz ticks)."""
+        n = C.c_uint32(0)
+        _check(_lib.rt_debug_stamps(self._h, None, 0, C.byref(n)))
+        out = np.zeros((n.value, 2), dtype=np.uint64)
+        _check(_lib.rt_debug_stamps(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), n.value, C.byref(n)))
+        return out
 
     def counters(self) -> dict:
         st = Stats()
