@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -18,6 +19,7 @@
 
 #include "../../include/rtc.h"
 #include "flop_model.hpp"
+#include "host_math.hpp"
 #include "rtc_internal.hpp"
 
 namespace rtc {
@@ -53,6 +55,7 @@ struct DeviceWorld {
     PatternRec<R>* patterns = nullptr;
     LightRec<R>* lights = nullptr;
     int32_t* world_slot = nullptr;
+    std::vector<std::array<double, 4>> bounds;  // host copy of ShapeRec::bound per slot (f64)
     DevScene<R> scene{};
     void release() {
         (void)hipFree(world_slot);
@@ -91,6 +94,7 @@ struct rt_context {
     uint32_t sched_pool = rtc::kSchedDynamic;
     bool staged_store = false;  // RTC_STAGED_STORE=1 stages tile pixels in LDS
     bool lds_world = true;      // RTC_LDS_WORLD=0 gathers shade data from global memory
+    double cull_coverage = rtc::kCullMaxCoverage;  // RTC_CULL_COVERAGE (negative: no cull in the first kCullSlots)
     size_t occ_lds[8] = {};     // occupancy cache: {direct,pool} x {f32,f64} x {global,LDS world}
     int occ_blocks[8] = {};
     unsigned long long* d_stamps = nullptr;  // RT_FLAG_STAMPS diagnostics
@@ -113,12 +117,100 @@ int upload(T** dst, const std::vector<T>& v) {
     return RT_OK;
 }
 
+// World-space bounding sphere of a shape's intersection set, for the
+// kernels' wave-level cull (wave_may_hit).  Acceleration only: a shape is
+// skipped for a wave only when no lane's ray can meet this sphere at t >= 0,
+// so it is padded well beyond the f32/f64 rounding of the local-space tests.
+// Returns radius -1 for unbounded shapes (planes, open-ended cylinders and
+// cones) and for transforms whose forward matrix is not finite.
+void bounding_sphere(const rt_shape_desc& d, double out[4]) {
+    out[0] = out[1] = out[2] = 0.0;
+    out[3] = -1.0;
+    double c[3] = {0.0, 0.0, 0.0}, r = 0.0;
+    const double lo = d.minimum, hi = d.maximum;
+    switch (d.kind) {
+        case RT_SHAPE_SPHERE: r = 1.0; break;
+        case RT_SHAPE_CUBE: r = std::sqrt(3.0); break;
+        case RT_SHAPE_CYLINDER:
+        case RT_SHAPE_CONE: {
+            if (!std::isfinite(lo) || !std::isfinite(hi) || !(lo <= hi)) return;
+            const double half = 0.5 * (hi - lo), rad2 = d.kind == RT_SHAPE_CYLINDER ? 1.0 : std::max(lo * lo, hi * hi);
+            c[1] = 0.5 * (lo + hi);
+            r = std::sqrt(rad2 + half * half);
+            break;
+        }
+        case RT_SHAPE_TRIANGLE: {
+            double p[3][3];
+            for (int q = 0; q < 3; ++q) {
+                p[0][q] = d.vertex_1[q];
+                p[1][q] = d.vertex_1[q] + d.edge_1[q];
+                p[2][q] = d.vertex_1[q] + d.edge_2[q];
+            }
+            for (int q = 0; q < 3; ++q) c[q] = (p[0][q] + p[1][q] + p[2][q]) / 3.0;
+            for (auto& v : p)
+                r = std::max(r, std::sqrt((v[0] - c[0]) * (v[0] - c[0]) + (v[1] - c[1]) * (v[1] - c[1]) +
+                                          (v[2] - c[2]) * (v[2] - c[2])));
+            break;
+        }
+        default: return;  // plane
+    }
+    hm::M4 inv;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) inv.m[i][j] = d.inverse[4 * i + j];
+    const hm::M4 f = hm::inverse(inv);
+    // spectral norm of the linear part <= sqrt(max abs row sum of F^T F)
+    double ftf[3][3] = {}, sigma2 = 0.0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) ftf[i][j] += f.m[k][i] * f.m[k][j];
+    for (auto& row : ftf) sigma2 = std::max(sigma2, std::fabs(row[0]) + std::fabs(row[1]) + std::fabs(row[2]));
+    double wc[3];
+    for (int i = 0; i < 3; ++i) wc[i] = f.m[i][0] * c[0] + f.m[i][1] * c[1] + f.m[i][2] * c[2] + f.m[i][3];
+    const double wr = r * std::sqrt(sigma2);
+    const double scale = std::fabs(wc[0]) + std::fabs(wc[1]) + std::fabs(wc[2]) + wr;
+    const double pad = 1e-3 * wr + 1e-4 * scale + 1e-4;
+    if (!std::isfinite(wc[0]) || !std::isfinite(wc[1]) || !std::isfinite(wc[2]) || !std::isfinite(wr) ||
+        wr + pad > 1e18)
+        return;
+    for (int i = 0; i < 3; ++i) out[i] = wc[i];
+    out[3] = wr + pad;
+}
+
+// Per-launch cull bits: a bounded shape keeps its wave cull unless its
+// padded bounding sphere covers more than kCullMaxCoverage of the view
+// (estimated as the disc area pi tan^2(angular radius) over the image plane
+// area at unit distance, 4 half_width half_height).  Without a camera
+// (color_at rays) every bounded shape culls.
+void cull_bits(const std::vector<std::array<double, 4>>& bounds, const rt_camera_desc* cam, double max_coverage,
+               uint32_t* bits) {
+    std::fill(bits, bits + kCullSlots / 32, 0u);
+    if (max_coverage < 0.0) return;
+    const double view = cam ? 4.0 * cam->half_width * cam->half_height : 0.0;
+    for (size_t i = 0; i < bounds.size() && i < (size_t)kCullSlots; ++i) {
+        const auto& b = bounds[i];
+        if (!(b[3] >= 0.0)) continue;
+        bool cull = true;
+        if (cam && view > 0.0) {
+            const double v[3] = {b[0] - cam->origin[0], b[1] - cam->origin[1], b[2] - cam->origin[2]};
+            const double dist2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2], r2 = b[3] * b[3];
+            if (dist2 <= r2) {
+                cull = false;  // the camera is inside the bound
+            } else {
+                const double tan2 = r2 / (dist2 - r2);
+                cull = 3.14159265358979 * tan2 / view <= max_coverage;
+            }
+        }
+        if (cull) bits[i >> 5] |= 1u << (i & 31);
+    }
+}
+
 template <typename R>
 int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes, uint32_t ns,
                 const rt_material_desc* mats, uint32_t nm, const rt_pattern_desc* pats, uint32_t np,
                 const rt_light_desc* lights, uint32_t nl) {
     (void)ctx;
     w.release();
+    w.bounds.clear();
     std::vector<ShapeRec<R>> sh;
     std::vector<int32_t> begin(kNumKinds + 1, 0);
     for (int k = 0; k < kNumKinds; ++k) {
@@ -128,6 +220,10 @@ int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes,
             if (d.kind != k) continue;
             ShapeRec<R> r{};
             for (int q = 0; q < 12; ++q) r.inv[q] = (R)d.inverse[q];
+            double bs[4];
+            bounding_sphere(d, bs);
+            for (int q = 0; q < 4; ++q) r.bound[q] = (R)bs[q];
+            w.bounds.push_back({bs[0], bs[1], bs[2], bs[3]});
             r.ymin = (R)d.minimum;
             r.ymax = (R)d.maximum;
             for (int q = 0; q < 3; ++q) {
@@ -290,6 +386,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
            hipStream_t stream, uint32_t flags = 0) {
     LaunchParams<R> P{};
     P.scene = w.scene;
+    cull_bits(w.bounds, cam, ctx->cull_coverage, P.scene.cull_bits);
     if (cam) {
         for (int q = 0; q < 12; ++q) P.cam.inv[q] = (R)cam->inverse[q];
         for (int q = 0; q < 3; ++q) P.cam.origin[q] = (R)cam->origin[q];
@@ -460,6 +557,7 @@ int rt_context_create(int device_ordinal, rt_context** out) {
     ctx->sched_pool = sched(std::getenv("RTC_SCHED_POOL"), ctx->sched_pool);
     if (const char* e = std::getenv("RTC_STAGED_STORE")) ctx->staged_store = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_LDS_WORLD")) ctx->lds_world = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("RTC_CULL_COVERAGE")) ctx->cull_coverage = std::atof(e);
     RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreate(&ctx->ev_start));
     RT_HIP(hipEventCreate(&ctx->ev_stop));

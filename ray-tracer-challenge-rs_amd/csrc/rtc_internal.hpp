@@ -46,6 +46,12 @@ constexpr int kDequeueChunkPool = 1;    // costly, high-variance tiles: balance 
 // World tables up to this size are staged into LDS for the per-lane gathers
 // (~120 f32 shapes); larger worlds gather from global memory (L2-resident).
 constexpr size_t kMaxWorldLds = 16 * 1024;
+// Wave cull (rtc_kernels.hip wave_may_hit) is decided per shape for the
+// first kCullSlots slots: a shape whose padded bounding sphere covers more
+// than kCullMaxCoverage of the camera's view is hit by most rays, so its
+// cull test would be pure overhead.
+constexpr int kCullSlots = 256;
+constexpr double kCullMaxCoverage = 1.0;
 
 // Fixed-point pixel accumulator of the pool kernel: contributions are summed
 // as int64 multiples of 2^-48 so the per-pixel sum is independent of the
@@ -57,6 +63,7 @@ template <typename R>
 struct alignas(16) ShapeRec {
     R inv[12];     // rows 0..2 of transformation_inverse (row 3 is never read:
                    // Mul<Point>/Mul<Vector> produce 3 rows, matrix.rs:332-362)
+    R bound[4];    // world bounding sphere (center, radius) for the wave cull; radius < 0 = unbounded
     R ymin, ymax;  // cylinder/cone min/max (cylinder.rs:12-14)
     R tri[12];     // triangle vertex_1, edge_1, edge_2, normal (triangle.rs:12-17)
     int32_t world_index;
@@ -123,6 +130,9 @@ struct DevScene {
     const PatternRec<R>* lpats;
     const int32_t* lworld_slot;
     int32_t kind_begin[kNumKinds + 1];
+    // Per-launch: slot s < kCullSlots runs the wave cull iff bit s is set
+    // (slots past kCullSlots always do).  Set by the host from the camera.
+    uint32_t cull_bits[kCullSlots / 32];
     int32_t n_materials, n_patterns;
     int32_t n_lights;
     int32_t any_secondary;  // some material has reflectiveness or transparency != 0

@@ -363,6 +363,34 @@ __device__ inline void for_all_kinds(const DevScene<R>& sc, F&& f) {
                                    [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_TRIANGLE>(s, i); });
 }
 
+// Wave-level cull (acceleration only): false when no active lane's ray
+// o + t d, t >= 0, can meet the shape's padded world bounding sphere
+// (rtc_host.cpp bounding_sphere), so the wave skips the shape; the reference
+// tests every shape (world.rs:25-35) and the set of hits at t >= 0 is the
+// same.  The ray meets the ball iff its line passes within r of the center,
+// |d x oc|^2 <= r^2 |d|^2, and the center is not behind an outside origin
+// (oc.d < 0 with |oc| > r makes |o + t d - C|^2 > r^2 for every t >= 0).
+// Not usable where t < 0 entries matter (the refractive-index walk).
+template <typename R>
+__device__ inline bool wave_may_hit(const DevScene<R>& sc, const ShapeRec<R>& s, int slot, V3<R> o, V3<R> d) {
+    const R r = s.bound[3];
+    if (!(r >= (R)0)) return true;  // unbounded shape: wave-uniform
+    if (slot < kCullSlots) {
+        // constant indices only: a dynamic one would demote the by-value
+        // DevScene to scratch memory
+        uint32_t word = 0;
+#pragma unroll
+        for (int q = 0; q < kCullSlots / 32; ++q) word = (slot >> 5) == q ? sc.cull_bits[q] : word;
+        if (!((word >> (slot & 31)) & 1u)) return true;
+    }
+    const V3<R> oc = {s.bound[0] - o.x, s.bound[1] - o.y, s.bound[2] - o.z};
+    const V3<R> c = cross(d, oc);
+    const R r2 = r * r;
+    const bool front = (dot(oc, d) >= (R)0) | (dot(oc, oc) <= r2);
+    const bool lane = front & (dot(c, c) <= r2 * dot(d, d));
+    return __ballot(lane) != 0;
+}
+
 template <typename R>
 struct Hit {
     R t;
@@ -380,7 +408,8 @@ template <typename R>
 __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
     R ht = Real<R>::kInf;
     int hw = INT_MAX;
-    for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int) {
+    for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
+        if (!wave_may_hit(sc, s, slot, o, d)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
         const int w = s.world_index;
@@ -404,8 +433,9 @@ __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
 template <typename R>
 __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) {
     bool hit = false;
-    for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int) {
+    for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
         if (!s.casts_shadow) return;  // wave-uniform
+        if (!wave_may_hit(sc, s, slot, o, d)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
         entries<R, K>(s, lo, ld, [&](R t, bool v) { hit |= v & (t >= (R)0) & (t < dist); });

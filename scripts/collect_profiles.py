@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Copy a round's rocprofv3 results from gpurun_out/ into profiles/ (tracked):
+kernel-trace stats CSVs, per-dispatch PMC averages, and profiles/traffic.json —
+HBM bytes per launch keyed by bench workload, computed as the guide prescribes
+(MI355X_MICROARCH.md "HBM": FETCH_SIZE/WRITE_SIZE are KiB; gfx950 FETCH_SIZE
+counts half of a wide streamed read, so it is doubled).
+
+Usage: python scripts/collect_profiles.py r01
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCENES = {"three_sphere": "three_sphere_scene@1920x1080,depth=6,f32",
+          "reflect_refract": "reflect_refract@1920x1080,depth=6,f32"}
+
+
+def pmc_means(d, pat="trace_"):
+    agg = collections.defaultdict(list)
+    for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
+        per = collections.defaultdict(float)
+        for r in csv.DictReader(open(f)):
+            if pat in r["Kernel_Name"]:
+                per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+        for (_, name), v in per.items():
+            agg[name].append(v)
+    return {k: sum(v) / len(v) for k, v in sorted(agg.items())}
+
+
+def main():
+    rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    tp = os.path.join(out, "traffic.json")
+    traffic = json.load(open(tp)) if os.path.exists(tp) else {}
+    for key, workload in SCENES.items():
+        src = os.path.join(ROOT, "gpurun_out", f"{rnd}_stats_{key}")
+        for f in glob.glob(os.path.join(src, "**", "*kernel_stats.csv"), recursive=True):
+            shutil.copy(f, os.path.join(out, f"{rnd}_kernel_stats_{key}.csv"))
+        log = os.path.join(src, "bench.log")
+        if os.path.exists(log):
+            lines = [l for l in open(log) if l.startswith("{")]
+            if lines:
+                open(os.path.join(out, f"{rnd}_bench_under_rocprof_{key}.json"), "w").write(lines[-1])
+        m = pmc_means(os.path.join(ROOT, "gpurun_out", f"{rnd}_pmc_{key}"))
+        if not m:
+            continue
+        if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+            hbm = (2 * m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024
+            m["hbm_bytes_per_launch"] = hbm
+            traffic[workload] = hbm
+        json.dump(m, open(os.path.join(out, f"{rnd}_pmc_{key}.json"), "w"), indent=1)
+        print(key, json.dumps(m))
+    json.dump(traffic, open(tp, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
