@@ -100,6 +100,7 @@ def main():
     import torch.distributed as dist
 
     import rtc_amd
+    from rtc_amd import dist as rdist
     from rtc_amd import scene_io
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,7 +119,7 @@ def main():
     rdtype = torch.float32 if args.precision == "f32" else torch.float64
     tiled = args.mode == "tiled" and world > 1
     if tiled:
-        rows = rtc_amd.shard_rows(cam.height, world)
+        rows = rdist.strip_height(cam.height, world)
         out = torch.empty((rows, cam.width, 3), dtype=rdtype, device="cuda")
         gathered = torch.empty((world * rows, cam.width, 3), dtype=rdtype, device="cuda") if rank == 0 else None
         image = torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda") if rank == 0 else None
@@ -129,8 +130,7 @@ def main():
     def step():
         ctx.render_device(cam, out.data_ptr(), sptr, args.depth, args.precision, "real", shard, args.flags)
         if tiled:
-            chunks = list(gathered.chunk(world)) if rank == 0 else None
-            dist.gather(out, chunks, dst=0)
+            rdist.gather_strips(out, gathered, world, rank)
             if rank == 0:
                 ctx.assemble_shards(gathered.data_ptr(), cam.width, cam.height, world, 3 * out.element_size(),
                                     image.data_ptr(), sptr)
@@ -159,15 +159,7 @@ def main():
 
     rays = after["rays"] - before["rays"]
     flops = after["algorithmic_flops"] - before["algorithmic_flops"]
-    t = torch.tensor([elapsed, rays], dtype=torch.float64, device="cuda")
-    if world > 1:
-        tmax = t[:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tot = t[1:].clone()
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        elapsed, total_rays = float(tmax.item()), float(tot.item())
-    else:
-        total_rays = float(rays)
+    elapsed, total_rays = rdist.job_totals(elapsed, rays, "cuda")
     if rank == 0:
         flops_per_launch = flops / args.steps
         achieved = flops_per_launch / (launch_ms * 1e-3) / 1e12

@@ -212,7 +212,9 @@ public:
     }
     Node parse_document() {
         size_t i = 0;
-        if (lines_.empty()) return Node{};  // empty stream: Yaml::BadValue-like, nothing to add
+        // yaml-rust yields no document for an empty stream and the reference
+        // asserts exactly one (scene_loader.rs:357)
+        if (lines_.empty()) fail("empty YAML stream (scene_loader.rs:357 expects one document)");
         Node n = block(i, lines_[0].indent);
         if (i != lines_.size()) fail("line " + std::to_string(lines_[i].lineno) + ": unexpected content");
         return n;

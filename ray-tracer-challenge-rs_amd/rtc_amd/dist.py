@@ -1,0 +1,77 @@
+"""Multi-GPU plumbing of the render path.
+
+Pixels are independent (camera.rs:106-110: every pixel is its own
+`color_at`), so the path shards without any data exchange:
+
+* frames mode: each rank renders whole frames; a job's throughput is the
+  rays of all ranks over the slowest rank's time (`job_totals`).  No
+  collective touches the data path.
+* tiled mode: ONE frame is split into cyclic RT_TILE_H-row blocks (block t
+  belongs to shard t % N, balancing rows of very different cost).  Shard s
+  renders its blocks, in order, into a contiguous strip of `strip_height`
+  rows (the last block may be clipped; strips are padded to equal height so
+  the gather has one send count), the strips are gathered to rank 0
+  (`gather_strips`, RCCL on GPUs / gloo in the CPU tests) and rank 0
+  de-interleaves them (`rt_assemble_shards` on the device; `assemble_host`
+  is its host mirror for tests).
+
+The scene needs no broadcast: it is a few KB every rank loads itself.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import RT_TILE_H, shard_rows
+
+
+def strip_height(height: int, shards: int) -> int:
+    """Rows of every shard's strip (rt_shard_rows)."""
+    return shard_rows(height, shards)
+
+
+def strip_canvas_rows(height: int, shards: int, shard: int) -> np.ndarray:
+    """Canvas row of each strip row of `shard`, in strip order; -1 marks the
+    padding rows past the canvas (never read by the assembly)."""
+    n_blocks = (height + RT_TILE_H - 1) // RT_TILE_H
+    rows = np.full(strip_height(height, shards), -1, dtype=np.int64)
+    k = 0
+    for t in range(shard, n_blocks, shards):
+        for w in range(RT_TILE_H):
+            y = t * RT_TILE_H + w
+            rows[k] = y if y < height else -1
+            k += 1
+    return rows
+
+
+def assemble_host(gathered: np.ndarray, height: int, shards: int) -> np.ndarray:
+    """Host mirror of rt_assemble_shards: gathered = shard-major strips
+    (shards * strip_height, W, C) -> (height, W, C) image."""
+    strip = strip_height(height, shards)
+    image = np.empty((height,) + gathered.shape[1:], dtype=gathered.dtype)
+    for s in range(shards):
+        rows = strip_canvas_rows(height, shards, s)
+        keep = rows >= 0
+        image[rows[keep]] = gathered[s * strip:(s + 1) * strip][keep]
+    return image
+
+
+def gather_strips(strip, gathered, world: int, rank: int, dst: int = 0) -> None:
+    """torch.distributed gather of equal-height strips to `dst`; `gathered`
+    is the (world * strip_height, W, C) receive buffer on `dst` (None elsewhere)."""
+    import torch.distributed as dist
+    chunks = list(gathered.chunk(world)) if rank == dst else None
+    dist.gather(strip, chunks, dst=dst)
+
+
+def job_totals(elapsed_s: float, rays: float, device) -> tuple[float, float]:
+    """(max elapsed over ranks, sum of rays over ranks): the whole-job
+    throughput is sum(rays) / max(elapsed)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(elapsed_s), float(rays)
+    t = torch.tensor([elapsed_s], dtype=torch.float64, device=device)
+    r = torch.tensor([rays], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(r, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(r.item())

@@ -1,0 +1,76 @@
+"""The `rtc` CLI (csrc/rtc_cli.cpp): the reference CLI's flow (main.rs:11-31,
+cli_arguments.rs:4-13) over the C-ABI — YAML in, 8-bit image out."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PKG
+
+CLI = os.path.join(PKG, "rtc_amd", "_lib", "rtc")
+
+SCENE = """
+- add: camera
+  width: 64
+  height: 48
+  field-of-view: 0.9
+  from: [0, 1.5, -5]
+  to: [0, 1, 0]
+  up: [0, 1, 0]
+- add: light
+  at: [-10, 10, -10]
+  intensity: [1, 1, 1]
+- add: plane
+  material:
+    pattern:
+      type: checkers
+      colors:
+        - [1, 1, 1]
+        - [0.1, 0.1, 0.1]
+    reflective: 0.3
+- add: sphere
+  transform:
+    - [translate, -0.5, 1, 0.5]
+  material:
+    color: [0.1, 0.2, 0.3]
+    transparency: 0.9
+    reflective: 0.9
+    refractive-index: 1.5
+- add: cube
+  transform:
+    - [scale, 0.4, 0.4, 0.4]
+    - [translate, 1.5, 0.4, -0.5]
+  material:
+    color: [1, 0.3, 0.2]
+"""
+
+
+def read_ppm(path):
+    data = open(path, "rb").read()
+    parts = data.split(b"\n", 3)
+    assert parts[0] == b"P6" and parts[2] == b"255"
+    w, h = map(int, parts[1].split())
+    return np.frombuffer(parts[3], dtype=np.uint8).reshape(h, w, 3)
+
+
+def test_cli_usage_and_missing_scene_fail_loudly(tmp_path):
+    assert subprocess.run([CLI], capture_output=True).returncode != 0
+    r = subprocess.run([CLI, str(tmp_path / "missing.yaml"), str(tmp_path / "o.ppm")], capture_output=True, text=True)
+    assert r.returncode != 0 and "error" in r.stderr
+
+
+@pytest.mark.gpu
+def test_cli_renders_the_scene_like_the_oracle(tmp_path, rtc, oracle):
+    yaml = tmp_path / "scene.yaml"
+    yaml.write_text(SCENE)
+    out = tmp_path / "out.ppm"
+    r = subprocess.run([CLI, str(yaml), str(out), "--precision", "f64", "--width", "80", "--height", "60"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "Image rendered in" in r.stdout
+    img = read_ppm(out)
+    scene = rtc.load_scene(str(yaml))
+    ref, _ = oracle.render(scene, rtc.camera_resize(scene.camera, 80, 60), 6)
+    d = np.abs(img.astype(int) - oracle.quantize(ref).astype(int))
+    assert d.max() <= 1 and (d == 0).mean() >= 0.999

@@ -1,0 +1,95 @@
+"""Multi-rank plumbing of the render path on CPU (gloo, world_size 2):
+row-block sharding, the strip gather and the de-interleave that bench.py's
+tiled mode runs over RCCL, plus the frames-mode job totals.
+
+The oracle stands in for the device renderer here (test infrastructure
+only): each rank renders exactly the canvas rows of its strip, so the
+assembled frame must equal the full-frame render bit for bit.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import scene_fixture
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _render_strip(oracle, scene, cam, rows):
+    strip = np.zeros((len(rows), cam.width, 3))
+    y = 0
+    while y < len(rows):
+        if rows[y] < 0:
+            y += 1
+            continue
+        y1 = y
+        while y1 < len(rows) and rows[y1] == rows[y] + (y1 - y):
+            y1 += 1
+        strip[y:y1], _ = oracle.render(scene, cam, 6, rows=(int(rows[y]), int(rows[y1 - 1]) + 1))
+        y = y1
+    return strip
+
+
+def _worker(rank, world, port, name, w, h, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    import pyoracle
+    import rtc_amd
+    from rtc_amd import dist as rdist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        scene = scene_fixture(name)
+        cam = rtc_amd.camera_resize(scene.camera, w, h)
+        rows = rdist.strip_canvas_rows(h, world, rank)
+        strip = torch.from_numpy(_render_strip(pyoracle, scene, cam, rows))
+        gathered = torch.empty((world * len(rows), w, 3), dtype=torch.float64) if rank == 0 else None
+        rdist.gather_strips(strip, gathered, world, rank)
+        elapsed, rays = rdist.job_totals(1.0 + rank, 100.0 * (rank + 1), "cpu")
+        if rank == 0:
+            image = rdist.assemble_host(gathered.numpy(), h, world)
+            np.savez(out_path, image=image, elapsed=elapsed, rays=rays)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,w,h", [("cover", 48, 37), ("three_sphere_scene", 40, 24)])
+def test_tiled_gather_reassembles_the_frame(tmp_path, oracle, rtc, name, w, h):
+    import torch.multiprocessing as mp
+    world = 2
+    out = str(tmp_path / "frame.npz")
+    mp.spawn(_worker, args=(world, _free_port(), name, w, h, out), nprocs=world, join=True)
+    res = np.load(out)
+    scene = scene_fixture(name)
+    ref, _ = oracle.render(scene, rtc.camera_resize(scene.camera, w, h), 6)
+    assert np.array_equal(res["image"], ref)
+    assert float(res["elapsed"]) == 2.0 and float(res["rays"]) == 300.0  # max time, summed rays
+
+
+@pytest.mark.parametrize("h,shards", [(1, 1), (5, 2), (37, 3), (1080, 8), (2160, 8), (7, 8)])
+def test_strip_rows_partition_the_canvas(h, shards):
+    from rtc_amd import dist as rdist
+    seen = np.concatenate([rdist.strip_canvas_rows(h, shards, s) for s in range(shards)])
+    assert sorted(seen[seen >= 0].tolist()) == list(range(h))
+    assert all(len(rdist.strip_canvas_rows(h, shards, s)) == rdist.strip_height(h, shards) for s in range(shards))
+
+
+def test_assemble_host_inverts_the_split():
+    from rtc_amd import dist as rdist
+    h, w, shards = 29, 5, 3
+    img = np.arange(h * w * 3, dtype=np.float32).reshape(h, w, 3)
+    strips = []
+    for s in range(shards):
+        rows = rdist.strip_canvas_rows(h, shards, s)
+        st = np.full((len(rows), w, 3), -1.0, dtype=np.float32)
+        st[rows >= 0] = img[rows[rows >= 0]]
+        strips.append(st)
+    assert np.array_equal(rdist.assemble_host(np.concatenate(strips), h, shards), img)

@@ -179,6 +179,62 @@ def test_pool_determinism_and_u8(gpu_ctx, rtc, oracle, name):
     assert np.array_equal(q, oracle.quantize(a.astype(np.float64)))
 
 
+def _render_with_env(rtc, monkeypatch, env, scene, cam, precision):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    with rtc.Context(0) as c:
+        c.upload(scene)
+        return c.render(cam, 6, precision=precision)
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+@pytest.mark.parametrize("name", ["three_sphere_scene", "shadow_puppets", "cover", "table", "cylinders", "metal"])
+def test_cull_is_exact(gpu_ctx, rtc, monkeypatch, name, precision):
+    """The wave cull is acceleration only: the frame with the cull off
+    (RTC_CULL_COVERAGE=-1) and forced on for every bounded shape (1e30)
+    equals the default frame bit for bit, counters included."""
+    scene = scene_fixture(name)
+    cam = rtc.camera_resize(scene.camera, 320, 200)
+    gpu_ctx.upload(scene)
+    a, sa = gpu_ctx.render(cam, 6, precision=precision)
+    for cov in ("-1", "1e30"):
+        b, sb = _render_with_env(rtc, monkeypatch, {"RTC_CULL_COVERAGE": cov}, scene, cam, precision)
+        assert np.array_equal(a, b), f"{name} {precision}: cull<={cov} changed {int((a != b).any(axis=2).sum())} px"
+        assert _counts(sa) == _counts(sb)
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_cull_is_exact_for_grazing_rays(gpu_ctx, rtc, monkeypatch, precision):
+    """Rays aimed within 1e-6 of sphere and cube silhouettes (rt_color_at
+    culls every bounded shape): identical with and without the cull."""
+    from rtc_amd import world as W
+    w = W.World([W.Light((-10, 10, -10))],
+                [W.sphere(W.Material(color=(1, 0.2, 0.2)), W.mat_mul(W.translation(0.3, 0.1, 0), W.scaling(0.7, 1.3, 0.9))),
+                 W.cube(W.Material(color=(0.2, 1, 0.2)), W.translation(2.5, 0, 0.5))])
+    tables = w.tables()
+    rng = np.random.default_rng(7)
+    n = 8192
+    o = rng.uniform(-6, 6, size=(n, 3))
+    o[:, 2] = -8
+    # targets on (or 1e-6 off) the unit sphere / cube surface in object space
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    u *= 1.0 + rng.choice([-1e-6, 0.0, 1e-6], size=(n, 1))
+    sph = np.array([0.3, 0.1, 0]) + u * np.array([0.7, 1.3, 0.9])
+    cub = np.array([2.5, 0, 0.5]) + np.clip(u * 1.8, -1 - 1e-6, 1 + 1e-6)
+    tgt = np.where(rng.random((n, 1)) < 0.5, sph, cub)
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([o, d], axis=1)
+    gpu_ctx.upload(tables)
+    a, sa = gpu_ctx.color_at(rays, precision=precision)
+    monkeypatch.setenv("RTC_CULL_COVERAGE", "-1")
+    with rtc.Context(0) as c:
+        c.upload(tables)
+        b, sb = c.color_at(rays, precision=precision)
+    assert np.array_equal(a, b) and _counts(sa) == _counts(sb)
+
+
 @pytest.mark.parametrize("shards", [2, 3, 8])
 def test_shards_reassemble_to_the_full_frame(gpu_ctx, rtc, shards):
     import torch
