@@ -41,8 +41,8 @@ PEAK_HBM_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--scene", default="three_sphere_scene")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -127,35 +127,51 @@ def main():
         out = torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda")
     shard = (rank, world) if tiled else (0, 1)
 
+    def gather():
+        rdist.gather_strips(out, gathered, world, rank)
+        if rank == 0:
+            ctx.assemble_shards(gathered.data_ptr(), cam.width, cam.height, world, 3 * out.element_size(),
+                                image.data_ptr(), sptr)
+
     def step():
         ctx.render_device(cam, out.data_ptr(), sptr, args.depth, args.precision, "real", shard, args.flags)
         if tiled:
-            rdist.gather_strips(out, gathered, world, rank)
-            if rank == 0:
-                ctx.assemble_shards(gathered.data_ptr(), cam.width, cam.height, world, 3 * out.element_size(),
-                                    image.data_ptr(), sptr)
+            gather()
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     before = ctx.counters()
 
-    # per-launch device time of the tracer kernel (HIP events on its stream)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # Device time of the tracer launches, from HIP events on the launch stream.
+    # Frames mode: ONE event pair brackets the K back-to-back launches (per-launch
+    # event records cost ~6 us of GPU time per frame on MI355X — they stop the
+    # next launch's waves from overlapping the previous one's tail — see
+    # scripts/host_overhead.py), so the average launch duration is the bracket
+    # / K.  Tiled mode: a pair around each render call, excluding the gather.
+    n_ev = args.steps if tiled else 1
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        step()
-        ev[i][1].record(stream)
+    if tiled:
+        for i in range(args.steps):
+            ev[i][0].record(stream)
+            ctx.render_device(cam, out.data_ptr(), sptr, args.depth, args.precision, "real", shard, args.flags)
+            ev[i][1].record(stream)
+            gather()
+    else:
+        ev[0][0].record(stream)
+        for _ in range(args.steps):
+            step()
+        ev[0][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     after = ctx.counters()
-    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    launch_ms = float(np.sum([a.elapsed_time(b) for a, b in ev])) / args.steps
 
     rays = after["rays"] - before["rays"]
     flops = after["algorithmic_flops"] - before["algorithmic_flops"]

@@ -384,10 +384,14 @@ __device__ inline bool wave_may_hit(const DevScene<R>& sc, const ShapeRec<R>& s,
         if (!((word >> (slot & 31)) & 1u)) return true;
     }
     const V3<R> oc = {s.bound[0] - o.x, s.bound[1] - o.y, s.bound[2] - o.z};
-    const V3<R> c = cross(d, oc);
-    const R r2 = r * r;
-    const bool front = (dot(oc, d) >= (R)0) | (dot(oc, oc) <= r2);
-    const bool lane = front & (dot(c, c) <= r2 * dot(d, d));
+    // |d x oc|^2 = |oc|^2 |d|^2 - (oc.d)^2 (Lagrange): reuses oc.d of the
+    // front test.  Rounding of the two products is bounded by ~12 ulp of
+    // |oc|^2 |d|^2; shrinking |oc|^2 by kCullSlack (>> that) keeps the test
+    // conservative, so no lane that meets the sphere is ever rejected.
+    constexpr R kCullSlack = sizeof(R) == 4 ? (R)1e-5 : (R)1e-12;
+    const R tc = dot(oc, d), oo = dot(oc, oc), r2 = r * r;
+    const bool front = (tc >= (R)0) | (oo <= r2);
+    const bool lane = front & ((oo * ((R)1 - kCullSlack) - r2) * dot(d, d) <= tc * tc);
     return __ballot(lane) != 0;
 }
 
@@ -874,8 +878,16 @@ __device__ inline DevScene<R> scene_view(const LaunchParams<R>& P, const ShapeRe
         const PatternRec<R>* __restrict__ patterns, const LightRec<R>* __restrict__ lights
 
 // --------------------------------------------------------------- kernels
+// Waves per SIMD the f32 direct kernel is register-limited to (VGPRs <= 512 /
+// waves).  Measured on MI355X, three_sphere 1080p (scripts/ab_builds.sh):
+// 7 (<= 72 VGPRs) 46.0 us, unconstrained (74 VGPRs, 6 waves) 46.5 us,
+// 8 (<= 64 VGPRs, spills at tile level) 48.9 us.
+#ifndef RTC_DIRECT_WAVES
+#define RTC_DIRECT_WAVES 7
+#endif
 template <typename R, bool kLds>
-__global__ __launch_bounds__(kBlock) void trace_direct(LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 4 ? RTC_DIRECT_WAVES : 1))) void trace_direct(
+    LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
     extern __shared__ __align__(16) unsigned char smem[];
     const DevScene<R> sc = scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem);
     if (P.stamps && threadIdx.x == 0) P.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();

@@ -116,7 +116,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def lib_path() -> str:
-    return os.path.join(_HERE, "_lib", "librtc.so")
+    # RTC_LIBRARY: an alternative in-tree build of the same ABI (A/B of build
+    # variants, scripts/ab_builds.sh); never a different implementation.
+    return os.environ.get("RTC_LIBRARY") or os.path.join(_HERE, "_lib", "librtc.so")
 
 
 def _load() -> C.CDLL:
