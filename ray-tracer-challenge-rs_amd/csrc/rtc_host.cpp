@@ -97,6 +97,9 @@ struct rt_context {
     double cull_coverage = rtc::kCullMaxCoverage;  // RTC_CULL_COVERAGE (negative: no cull in the first kCullSlots)
     size_t occ_lds[8] = {};     // occupancy cache: {direct,pool} x {f32,f64} x {global,LDS world}
     int occ_blocks[8] = {};
+    uint32_t pool_lds_rays = 0;  // RTC_POOL_LDS_RAYS: LDS-resident pool slots (0 = sized for occupancy)
+    void* d_spill = nullptr;     // ray-pool overflow regions, one per resident workgroup
+    size_t spill_bytes = 0;
     unsigned long long* d_stamps = nullptr;  // RT_FLAG_STAMPS diagnostics
     uint32_t stamp_capacity = 0, stamp_count = 0;
     void* d_scratch = nullptr;  // host-buffer renders / color_at staging
@@ -342,8 +345,52 @@ struct LaunchShape {
     uint32_t sched;
     uint32_t grid;
     size_t lds;
-    uint32_t cap, batch;
+    uint32_t cap, lcap, batch;  // pool: LIFO bound, its LDS-resident part, pop batch
 };
+
+// Cached occupancy (workgroups per CU) of one kernel instantiation at a
+// given dynamic LDS size.
+template <typename R>
+int blocks_per_cu(rt_context* ctx, bool pool, bool lds_world, size_t lds, int* per_cu) {
+    const int key = (pool ? 1 : 0) + (sizeof(R) == 8 ? 2 : 0) + (lds_world ? 4 : 0);
+    if (ctx->occ_lds[key] == lds && ctx->occ_blocks[key] > 0) {
+        *per_cu = ctx->occ_blocks[key];
+        return RT_OK;
+    }
+    RT_HIP(occupancy<R>(pool, lds_world, lds, per_cu));
+    ctx->occ_lds[key] = lds;
+    ctx->occ_blocks[key] = *per_cu;
+    return RT_OK;
+}
+
+// LDS-resident part of the ray pool: as many slots as keep the pool kernel
+// at the workgroups/CU its registers allow (4 for f32 at <= 128 VGPRs, vs 2
+// when the whole LIFO bound sat in LDS); the rest of the bound spills to
+// global memory.  RTC_POOL_LDS_RAYS overrides (A/B).
+template <typename R>
+int pool_lds_rays(rt_context* ctx, uint32_t world_lds, uint32_t cap, uint32_t* lcap) {
+    if (ctx->pool_lds_rays > 0) {
+        *lcap = std::min<uint32_t>(cap, std::max<uint32_t>(kBlock, ctx->pool_lds_rays));
+        return RT_OK;
+    }
+    const bool lw = world_lds != 0;
+    int best = 0, rc;
+    if ((rc = blocks_per_cu<R>(ctx, true, lw, world_lds + pool_lds_bytes<R>(kBlock), &best))) return rc;
+    if (best < 1) best = 1;
+    const size_t rec = 7 * sizeof(R) + sizeof(uint32_t);
+    const size_t budget = 160 * 1024 / (size_t)best;
+    const size_t fixed = world_lds + pool_lds_bytes<R>(0);
+    uint32_t n = budget > fixed ? (uint32_t)((budget - fixed) / rec) : kBlock;
+    n = std::min<uint32_t>(cap, std::max<uint32_t>(kBlock, n & ~31u));
+    for (;;) {  // static LDS (tile staging) is not in `fixed`: step down until it fits
+        int got = 0;
+        if ((rc = blocks_per_cu<R>(ctx, true, lw, world_lds + pool_lds_bytes<R>(n), &got))) return rc;
+        if (got >= best || n <= (uint32_t)kBlock) break;
+        n = std::max<uint32_t>(kBlock, n - 32);
+    }
+    *lcap = n;
+    return RT_OK;
+}
 
 template <typename R>
 int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t n_tiles, LaunchShape& ls) {
@@ -351,31 +398,31 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
     const size_t wb = world_lds_bytes<R>(sc.kind_begin[kNumKinds], sc.n_materials, sc.n_patterns);
     ls.world_lds = (ctx->lds_world && wb <= kMaxWorldLds) ? (uint32_t)wb : 0;
     ls.lds = ls.world_lds;
-    ls.cap = ls.batch = 0;
+    ls.cap = ls.lcap = ls.batch = 0;
+    ls.sched = ls.pool ? ctx->sched_pool : (ctx->sched_direct == kSchedDynamic ? kSchedStatic : ctx->sched_direct);
+    int rc;
     if (ls.pool) {
-        const size_t room = kMaxLds - ls.world_lds;
-        uint32_t batch = kBlock;
-        while (batch > 32 && pool_lds_bytes<R>(pool_capacity(depth, batch)) > room) batch /= 2;
-        if (pool_lds_bytes<R>(pool_capacity(depth, batch)) > room)
-            return set_error(RT_ERR_INVALID, "max_depth too large for the LDS ray pool");
-        ls.batch = batch;
-        ls.cap = pool_capacity(depth, batch);
-        ls.lds += pool_lds_bytes<R>(ls.cap);
+        if (ls.sched == kSchedGrid) {
+            // one workgroup per tile: no per-workgroup spill region, so the
+            // whole LIFO bound lives in LDS (smaller pop batches if needed)
+            const size_t room = kMaxLds - ls.world_lds;
+            uint32_t batch = kBlock;
+            while (batch > 32 && pool_lds_bytes<R>(pool_capacity(depth, batch)) > room) batch /= 2;
+            if (pool_lds_bytes<R>(pool_capacity(depth, batch)) > room)
+                return set_error(RT_ERR_INVALID, "max_depth too large for the LDS ray pool");
+            ls.batch = batch;
+            ls.cap = ls.lcap = pool_capacity(depth, batch);
+        } else {
+            ls.batch = kBlock;
+            ls.cap = pool_capacity(depth, kBlock);
+            if ((rc = pool_lds_rays<R>(ctx, ls.world_lds, ls.cap, &ls.lcap))) return rc;
+        }
+        ls.lds += pool_lds_bytes<R>(ls.lcap);
     }
-    const int key = (ls.pool ? 1 : 0) + (sizeof(R) == 8 ? 2 : 0) + (ls.world_lds ? 4 : 0);
     int per_cu = 0;
-    if (ctx->occ_lds[key] == ls.lds && ctx->occ_blocks[key] > 0) {
-        per_cu = ctx->occ_blocks[key];
-    } else {
-        RT_HIP(occupancy<R>(ls.pool, ls.world_lds != 0, ls.lds, &per_cu));
-        ctx->occ_lds[key] = ls.lds;
-        ctx->occ_blocks[key] = per_cu;
-    }
+    if ((rc = blocks_per_cu<R>(ctx, ls.pool, ls.world_lds != 0, ls.lds, &per_cu))) return rc;
     if (per_cu < 1) per_cu = 1;
     const uint64_t resident = (uint64_t)per_cu * (uint64_t)ctx->cu_count;
-    // The direct kernel has no tile queue (its tiles cost the same): a
-    // dynamic request runs as the static persistent grid.
-    ls.sched = ls.pool ? ctx->sched_pool : (ctx->sched_direct == kSchedDynamic ? kSchedStatic : ctx->sched_direct);
     ls.grid = ls.sched != kSchedGrid ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, resident)) : n_tiles;
     return RT_OK;
 }
@@ -416,7 +463,19 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     int rc = plan_launch<R>(ctx, w.scene, depth, P.n_tiles, ls);
     if (rc) return rc;
     P.pool_capacity = ls.cap;
+    P.pool_lds_capacity = ls.lcap;
     P.pop_batch = ls.batch;
+    if (ls.cap > ls.lcap) {
+        const size_t need = (size_t)ls.grid * 8 * (ls.cap - ls.lcap) * sizeof(R);
+        if (ctx->spill_bytes < need) {
+            (void)hipFree(ctx->d_spill);
+            ctx->d_spill = nullptr;
+            ctx->spill_bytes = 0;
+            RT_HIP(hipMalloc(&ctx->d_spill, need));
+            ctx->spill_bytes = need;
+        }
+        P.spill = ctx->d_spill;
+    }
     P.persistent = ls.sched;
     P.dequeue_chunk = ls.pool ? kDequeueChunkPool : kDequeueChunkDirect;
     P.staged_store = ctx->staged_store ? 1 : 0;
@@ -558,6 +617,7 @@ int rt_context_create(int device_ordinal, rt_context** out) {
     if (const char* e = std::getenv("RTC_STAGED_STORE")) ctx->staged_store = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_LDS_WORLD")) ctx->lds_world = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_CULL_COVERAGE")) ctx->cull_coverage = std::atof(e);
+    if (const char* e = std::getenv("RTC_POOL_LDS_RAYS")) ctx->pool_lds_rays = (uint32_t)std::atoi(e);
     RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreate(&ctx->ev_start));
     RT_HIP(hipEventCreate(&ctx->ev_stop));
@@ -583,6 +643,7 @@ int rt_context_destroy(rt_context* ctx) {
     (void)hipFree(ctx->d_error);
     (void)hipFree(ctx->d_scratch);
     (void)hipFree(ctx->d_stamps);
+    (void)hipFree(ctx->d_spill);
     if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
     if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

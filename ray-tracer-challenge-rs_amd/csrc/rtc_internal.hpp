@@ -153,13 +153,15 @@ struct LaunchParams {
     uint32_t shard_index, shard_count;
     uint32_t n_tiles;        // tiles_x * tile_rows (or ray chunks in color_at mode)
     uint32_t max_depth;      // `remaining` of the primary ray
-    uint32_t pool_capacity;  // pool kernel: rays held in LDS
+    uint32_t pool_capacity;  // pool kernel: LIFO bound (rays) per workgroup
+    uint32_t pool_lds_capacity;  // of which held in LDS; the rest in `spill`
     uint32_t pop_batch;      // pool kernel: rays popped per iteration (<= kBlock)
     uint32_t persistent;     // kSched*: tile scheduling of this launch
     uint32_t dequeue_chunk;  // tiles per dequeue (persistent mode)
     uint32_t staged_store;   // stage tile pixels in LDS for contiguous stores
     uint32_t flags;          // RT_FLAG_* diagnostic ablations
     uint32_t world_lds;      // bytes of world tables staged at the start of dynamic LDS (0 = none)
+    void* spill;                 // pool overflow: grid x 8 x (pool_capacity - pool_lds_capacity) words
     unsigned long long* stamps;  // RT_FLAG_STAMPS: 2 x grid s_memrealtime values
     unsigned long long* tile_counter;  // kTileQueues cumulative dequeue counters (one per XCD)
     unsigned long long tile_base[kTileQueues];  // their values at this launch's start

@@ -370,7 +370,8 @@ __device__ inline void for_all_kinds(const DevScene<R>& sc, F&& f) {
 // same.  The ray meets the ball iff its line passes within r of the center,
 // |d x oc|^2 <= r^2 |d|^2, and the center is not behind an outside origin
 // (oc.d < 0 with |oc| > r makes |o + t d - C|^2 > r^2 for every t >= 0).
-// Not usable where t < 0 entries matter (the refractive-index walk).
+// Not used by the refractive-index walk (it counts t < 0 entries; a
+// line-only variant measured slower there: its transparent shapes are large).
 template <typename R>
 __device__ inline bool wave_may_hit(const DevScene<R>& sc, const ShapeRec<R>& s, int slot, V3<R> o, V3<R> d) {
     const R r = s.bound[3];
@@ -932,12 +933,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     }
 }
 
-// Ray pool layout in dynamic LDS: [acc: 3 x kBlock i64][ox oy oz dx dy dz w : cap x R][meta : cap x u32]
+// Ray pool: a LIFO of pending rays per workgroup.  Slots [0, lds_cap) live
+// in dynamic LDS after the world tables:
+//   [acc: 3 x kBlock i64][ox oy oz dx dy dz w : lds_cap x R][meta : lds_cap x u32]
+// and slots [lds_cap, cap) in this workgroup's region of P.spill (same SoA
+// layout, cap - lds_cap entries per array).  The LIFO bound cap = P + depth x
+// batch is what makes overflow impossible; the LDS part is sized for
+// occupancy (rtc_host.cpp plan_launch), the rare deep excursions spill.
 template <typename R>
 struct Pool {
     long long* acc;
-    R *ox, *oy, *oz, *dx, *dy, *dz, *w;
-    uint32_t* meta;  // pixel (bits 0-7) | remaining << 8
+    R* lds;    // 8 arrays of lds_cap words: ox oy oz dx dy dz w, then meta (u32)
+    R* spill;  // 8 arrays of spill_cap words (this workgroup's region)
+    int lds_cap, spill_cap;
 };
 
 // Reserve `pred` slots for the lanes of one wave: ballot + mbcnt prefix, one
@@ -953,16 +961,55 @@ __device__ inline int wave_reserve(bool pred, int* top) {
     return pred ? base + prefix : -1;
 }
 
+// One base pointer and a stride per level (not 16 pointers: those were
+// kept in VGPRs and spilled to scratch), and one branch per level so each
+// side keeps its address space (ds_* for LDS, global_* for the spill; a
+// pointer that may be either becomes flat_*).  meta = pixel | remaining << 8.
+#define RTC_AS_LDS __attribute__((address_space(3)))
+#define RTC_AS_GLOBAL __attribute__((address_space(1)))
+
+template <typename R, typename PR, typename PU>
+__device__ inline void pool_store(PR base, PU metas, int n, int i, V3<R> o, V3<R> d, R w, uint32_t meta) {
+    base[i] = o.x;
+    base[n + i] = o.y;
+    base[2 * n + i] = o.z;
+    base[3 * n + i] = d.x;
+    base[4 * n + i] = d.y;
+    base[5 * n + i] = d.z;
+    base[6 * n + i] = w;
+    metas[i] = meta;
+}
+
+template <typename R, typename PR, typename PU>
+__device__ inline void pool_load(PR base, PU metas, int n, int i, V3<R>& o, V3<R>& d, R& w, uint32_t& meta) {
+    o = {base[i], base[n + i], base[2 * n + i]};
+    d = {base[3 * n + i], base[4 * n + i], base[5 * n + i]};
+    w = base[6 * n + i];
+    meta = metas[i];
+}
+
 template <typename R>
 __device__ inline void pool_put(const Pool<R>& pl, int slot, V3<R> o, V3<R> d, R w, uint32_t meta) {
-    pl.ox[slot] = o.x;
-    pl.oy[slot] = o.y;
-    pl.oz[slot] = o.z;
-    pl.dx[slot] = d.x;
-    pl.dy[slot] = d.y;
-    pl.dz[slot] = d.z;
-    pl.w[slot] = w;
-    pl.meta[slot] = meta;
+    if (slot < pl.lds_cap) {
+        RTC_AS_LDS R* b = (RTC_AS_LDS R*)pl.lds;
+        pool_store<R>(b, (RTC_AS_LDS uint32_t*)(b + 7 * pl.lds_cap), pl.lds_cap, slot, o, d, w, meta);
+    } else {
+        RTC_AS_GLOBAL R* b = (RTC_AS_GLOBAL R*)pl.spill;
+        pool_store<R>(b, (RTC_AS_GLOBAL uint32_t*)(b + 7 * pl.spill_cap), pl.spill_cap, slot - pl.lds_cap, o, d,
+                      w, meta);
+    }
+}
+
+template <typename R>
+__device__ inline void pool_get(const Pool<R>& pl, int slot, V3<R>& o, V3<R>& d, R& w, uint32_t& meta) {
+    if (slot < pl.lds_cap) {
+        const RTC_AS_LDS R* b = (const RTC_AS_LDS R*)pl.lds;
+        pool_load<R>(b, (const RTC_AS_LDS uint32_t*)(b + 7 * pl.lds_cap), pl.lds_cap, slot, o, d, w, meta);
+    } else {
+        const RTC_AS_GLOBAL R* b = (const RTC_AS_GLOBAL R*)pl.spill;
+        pool_load<R>(b, (const RTC_AS_GLOBAL uint32_t*)(b + 7 * pl.spill_cap), pl.spill_cap, slot - pl.lds_cap, o, d,
+                     w, meta);
+    }
 }
 
 __device__ inline void acc_add(long long* acc, uint32_t pix, double v) {
@@ -980,17 +1027,14 @@ __global__ __launch_bounds__(kBlock) void trace_pool(LaunchParams<R> P, RTC_WORL
     __shared__ int s_top[2];
     __shared__ R s_px[3 * kBlock];
     const uint32_t cap = P.pool_capacity;
+    const uint32_t lcap = P.pool_lds_capacity, gcap = cap - lcap;
     Pool<R> pl;
     pl.acc = reinterpret_cast<long long*>(smem);
-    R* base = reinterpret_cast<R*>(smem + 3 * kBlock * sizeof(long long));
-    pl.ox = base;
-    pl.oy = base + cap;
-    pl.oz = base + 2 * cap;
-    pl.dx = base + 3 * cap;
-    pl.dy = base + 4 * cap;
-    pl.dz = base + 5 * cap;
-    pl.w = base + 6 * cap;
-    pl.meta = reinterpret_cast<uint32_t*>(base + 7 * cap);
+    pl.lds = reinterpret_cast<R*>(smem + 3 * kBlock * sizeof(long long));
+    pl.lds_cap = (int)lcap;
+    // 8 words per spilled entry; blockIdx.x < grid (persistent launch)
+    pl.spill = reinterpret_cast<R*>(P.spill) + (size_t)blockIdx.x * 8 * gcap;
+    pl.spill_cap = (int)gcap;
 
     Counts k = {};
     const uint32_t tid = threadIdx.x;
@@ -1025,13 +1069,7 @@ __global__ __launch_bounds__(kBlock) void trace_pool(LaunchParams<R> P, RTC_WORL
             V3<R> ro, rd;
             R rw = (R)0;
             uint32_t meta = 0;
-            if (active) {
-                const int sl = bottom + (int)tid;
-                ro = {pl.ox[sl], pl.oy[sl], pl.oz[sl]};
-                rd = {pl.dx[sl], pl.dy[sl], pl.dz[sl]};
-                rw = pl.w[sl];
-                meta = pl.meta[sl];
-            }
+            if (active) pool_get(pl, bottom + (int)tid, ro, rd, rw, meta);
             if (tid == 0) s_top[cur ^ 1] = bottom;
             __syncthreads();  // every lane holds its ray; the next top is set
             Shaded<R> sh;
