@@ -179,15 +179,14 @@ void bounding_sphere(const rt_shape_desc& d, double out[4]) {
     out[3] = wr + pad;
 }
 
-// Per-launch cull bits: a bounded shape keeps its wave cull unless its
+// Per-launch cull mask: a bounded shape keeps its wave cull unless its
 // padded bounding sphere covers more than kCullMaxCoverage of the view
 // (estimated as the disc area pi tan^2(angular radius) over the image plane
 // area at unit distance, 4 half_width half_height).  Without a camera
 // (color_at rays) every bounded shape culls.
-void cull_bits(const std::vector<std::array<double, 4>>& bounds, const rt_camera_desc* cam, double max_coverage,
-               uint32_t* bits) {
-    std::fill(bits, bits + kCullSlots / 32, 0u);
-    if (max_coverage < 0.0) return;
+uint64_t cull_mask(const std::vector<std::array<double, 4>>& bounds, const rt_camera_desc* cam, double max_coverage) {
+    uint64_t bits = 0;
+    if (max_coverage < 0.0) return 0;
     const double view = cam ? 4.0 * cam->half_width * cam->half_height : 0.0;
     for (size_t i = 0; i < bounds.size() && i < (size_t)kCullSlots; ++i) {
         const auto& b = bounds[i];
@@ -203,8 +202,9 @@ void cull_bits(const std::vector<std::array<double, 4>>& bounds, const rt_camera
                 cull = 3.14159265358979 * tan2 / view <= max_coverage;
             }
         }
-        if (cull) bits[i >> 5] |= 1u << (i & 31);
+        if (cull) bits |= 1ull << i;
     }
+    return bits;
 }
 
 template <typename R>
@@ -225,7 +225,8 @@ int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes,
             for (int q = 0; q < 12; ++q) r.inv[q] = (R)d.inverse[q];
             double bs[4];
             bounding_sphere(d, bs);
-            for (int q = 0; q < 4; ++q) r.bound[q] = (R)bs[q];
+            for (int q = 0; q < 3; ++q) r.bound[q] = (R)bs[q];
+            r.bound[3] = bs[3] >= 0.0 ? (R)(bs[3] * bs[3]) : (R)-1;  // device keeps r^2
             w.bounds.push_back({bs[0], bs[1], bs[2], bs[3]});
             r.ymin = (R)d.minimum;
             r.ymax = (R)d.maximum;
@@ -433,7 +434,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
            hipStream_t stream, uint32_t flags = 0) {
     LaunchParams<R> P{};
     P.scene = w.scene;
-    cull_bits(w.bounds, cam, ctx->cull_coverage, P.scene.cull_bits);
+    P.scene.cull_mask = cull_mask(w.bounds, cam, ctx->cull_coverage);
     if (cam) {
         for (int q = 0; q < 12; ++q) P.cam.inv[q] = (R)cam->inverse[q];
         for (int q = 0; q < 3; ++q) P.cam.origin[q] = (R)cam->origin[q];

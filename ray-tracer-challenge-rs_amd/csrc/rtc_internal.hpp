@@ -50,7 +50,7 @@ constexpr size_t kMaxWorldLds = 16 * 1024;
 // first kCullSlots slots: a shape whose padded bounding sphere covers more
 // than kCullMaxCoverage of the camera's view is hit by most rays, so its
 // cull test would be pure overhead.
-constexpr int kCullSlots = 256;
+constexpr int kCullSlots = 64;
 constexpr double kCullMaxCoverage = 1.0;
 
 // Fixed-point pixel accumulator of the pool kernel: contributions are summed
@@ -63,7 +63,7 @@ template <typename R>
 struct alignas(16) ShapeRec {
     R inv[12];     // rows 0..2 of transformation_inverse (row 3 is never read:
                    // Mul<Point>/Mul<Vector> produce 3 rows, matrix.rs:332-362)
-    R bound[4];    // world bounding sphere (center, radius) for the wave cull; radius < 0 = unbounded
+    R bound[4];    // world bounding sphere (center, radius^2) for the wave cull; < 0 = unbounded
     R ymin, ymax;  // cylinder/cone min/max (cylinder.rs:12-14)
     R tri[12];     // triangle vertex_1, edge_1, edge_2, normal (triangle.rs:12-17)
     int32_t world_index;
@@ -132,7 +132,9 @@ struct DevScene {
     int32_t kind_begin[kNumKinds + 1];
     // Per-launch: slot s < kCullSlots runs the wave cull iff bit s is set
     // (slots past kCullSlots always do).  Set by the host from the camera.
-    uint32_t cull_bits[kCullSlots / 32];
+    // One 64-bit mask: a shift and an AND in SGPRs per shape test (an array
+    // needed a compare/select chain, ~16 SALU per test).
+    uint64_t cull_mask;
     int32_t n_materials, n_patterns;
     int32_t n_lights;
     int32_t any_secondary;  // some material has reflectiveness or transparency != 0

@@ -372,28 +372,25 @@ __device__ inline void for_all_kinds(const DevScene<R>& sc, F&& f) {
 // (oc.d < 0 with |oc| > r makes |o + t d - C|^2 > r^2 for every t >= 0).
 // Not used by the refractive-index walk (it counts t < 0 entries; a
 // line-only variant measured slower there: its transparent shapes are large).
+// Wave-wide OR of a lane predicate (active lanes).  The raw builtin: HIP's
+// __ballot(int) turns the predicate into a VGPR and compares it again.
+__device__ inline bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+
 template <typename R>
 __device__ inline bool wave_may_hit(const DevScene<R>& sc, const ShapeRec<R>& s, int slot, V3<R> o, V3<R> d) {
-    const R r = s.bound[3];
-    if (!(r >= (R)0)) return true;  // unbounded shape: wave-uniform
-    if (slot < kCullSlots) {
-        // constant indices only: a dynamic one would demote the by-value
-        // DevScene to scratch memory
-        uint32_t word = 0;
-#pragma unroll
-        for (int q = 0; q < kCullSlots / 32; ++q) word = (slot >> 5) == q ? sc.cull_bits[q] : word;
-        if (!((word >> (slot & 31)) & 1u)) return true;
-    }
+    const R r2 = s.bound[3];  // radius^2
+    if (!(r2 >= (R)0)) return true;  // unbounded shape: wave-uniform
+    if (slot < kCullSlots && !((sc.cull_mask >> slot) & 1ull)) return true;
     const V3<R> oc = {s.bound[0] - o.x, s.bound[1] - o.y, s.bound[2] - o.z};
     // |d x oc|^2 = |oc|^2 |d|^2 - (oc.d)^2 (Lagrange): reuses oc.d of the
     // front test.  Rounding of the two products is bounded by ~12 ulp of
     // |oc|^2 |d|^2; shrinking |oc|^2 by kCullSlack (>> that) keeps the test
     // conservative, so no lane that meets the sphere is ever rejected.
-    constexpr R kCullSlack = sizeof(R) == 4 ? (R)1e-5 : (R)1e-12;
-    const R tc = dot(oc, d), oo = dot(oc, oc), r2 = r * r;
+    constexpr R kKeep = sizeof(R) == 4 ? (R)(1 - 1e-5) : (R)(1 - 1e-12);
+    const R tc = dot(oc, d), oo = dot(oc, oc);
     const bool front = (tc >= (R)0) | (oo <= r2);
-    const bool lane = front & ((oo * ((R)1 - kCullSlack) - r2) * dot(d, d) <= tc * tc);
-    return __ballot(lane) != 0;
+    const bool lane = front & (Real<R>::madd(oo, kKeep, -r2) * dot(d, d) <= tc * tc);
+    return wave_any(lane);
 }
 
 template <typename R>
@@ -951,7 +948,7 @@ struct Pool {
 // Reserve `pred` slots for the lanes of one wave: ballot + mbcnt prefix, one
 // LDS atomic per wave.  Returns the lane's slot or -1.
 __device__ inline int wave_reserve(bool pred, int* top) {
-    const unsigned long long m = __ballot(pred);
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(pred);
     if (m == 0) return -1;
     const int prefix = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
     const int leader = __ffsll((long long)m) - 1;
