@@ -97,6 +97,7 @@ struct rt_context {
     double cull_coverage = rtc::kCullMaxCoverage;  // RTC_CULL_COVERAGE (negative: no cull in the first kCullSlots)
     size_t occ_lds[8] = {};     // occupancy cache: {direct,pool} x {f32,f64} x {global,LDS world}
     int occ_blocks[8] = {};
+    uint32_t direct_grid = 0;    // RTC_DIRECT_GRID: persistent grid size of the direct kernel (0 = resident)
     uint32_t pool_lds_rays = 0;  // RTC_POOL_LDS_RAYS: LDS-resident pool slots (0 = sized for occupancy)
     void* d_spill = nullptr;     // ray-pool overflow regions, one per resident workgroup
     size_t spill_bytes = 0;
@@ -425,6 +426,8 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
     if (per_cu < 1) per_cu = 1;
     const uint64_t resident = (uint64_t)per_cu * (uint64_t)ctx->cu_count;
     ls.grid = ls.sched != kSchedGrid ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, resident)) : n_tiles;
+    if (!ls.pool && ls.sched == kSchedStatic && ctx->direct_grid > 0)  // RTC_DIRECT_GRID (A/B)
+        ls.grid = std::min<uint32_t>(n_tiles, ctx->direct_grid);
     return RT_OK;
 }
 
@@ -619,6 +622,7 @@ int rt_context_create(int device_ordinal, rt_context** out) {
     if (const char* e = std::getenv("RTC_LDS_WORLD")) ctx->lds_world = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_CULL_COVERAGE")) ctx->cull_coverage = std::atof(e);
     if (const char* e = std::getenv("RTC_POOL_LDS_RAYS")) ctx->pool_lds_rays = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("RTC_DIRECT_GRID")) ctx->direct_grid = (uint32_t)std::atoi(e);
     RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreate(&ctx->ev_start));
     RT_HIP(hipEventCreate(&ctx->ev_stop));

@@ -64,12 +64,15 @@ struct alignas(16) ShapeRec {
     R inv[12];     // rows 0..2 of transformation_inverse (row 3 is never read:
                    // Mul<Point>/Mul<Vector> produce 3 rows, matrix.rs:332-362)
     R bound[4];    // world bounding sphere (center, radius^2) for the wave cull; < 0 = unbounded
-    R ymin, ymax;  // cylinder/cone min/max (cylinder.rs:12-14)
-    R tri[12];     // triangle vertex_1, edge_1, edge_2, normal (triangle.rs:12-17)
+    // Right after inv/bound so one scalar-load burst at the top of a shape
+    // iteration covers everything a sphere/plane/cube test reads (a later
+    // world_index load cost a second s_waitcnt per iteration).
     int32_t world_index;
+    int32_t casts_shadow;  // material.casts_shadow, hoisted for the any-hit loop
     int32_t material;
     int32_t closed;
-    int32_t casts_shadow;  // material.casts_shadow, hoisted for the any-hit loop
+    R ymin, ymax;  // cylinder/cone min/max (cylinder.rs:12-14)
+    R tri[12];     // triangle vertex_1, edge_1, edge_2, normal (triangle.rs:12-17)
 };
 
 template <typename R>

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--precision", default="f32")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--out", default="real", choices=["real", "u8"])
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -32,10 +33,10 @@ def main():
     cam = rtc_amd.camera_resize(scene.camera, args.width, args.height)
     ctx = rtc_amd.Context(0)
     ctx.upload(scene)
-    out = torch.empty((cam.height, cam.width, 3), dtype=torch.float32 if args.precision == "f32" else torch.float64,
-                      device="cuda")
+    dt = torch.uint8 if args.out == "u8" else (torch.float32 if args.precision == "f32" else torch.float64)
+    out = torch.empty((cam.height, cam.width, 3), dtype=dt, device="cuda")
     for _ in range(5):
-        ctx.render_device(cam, out.data_ptr(), 0, 6, args.precision, "real", (0, 1), args.flags | 8)
+        ctx.render_device(cam, out.data_ptr(), 0, 6, args.precision, args.out, (0, 1), args.flags | 8)
     torch.cuda.synchronize()
     st = ctx.debug_stamps().astype(np.int64)
     t0 = st[:, 0].min()
@@ -43,7 +44,15 @@ def main():
     end = (st[:, 1] - t0) * 10e-3
     dur = end - start
     q = lambda a: [round(float(np.quantile(a, p)), 2) for p in (0, 0.1, 0.5, 0.9, 1.0)]  # noqa: E731
-    res = {"label": f"{args.scene} flags={args.flags} sched={os.environ.get('RTC_SCHED_DIRECT', 'default')}",
+    # kernel-only time of the same launch without stamps, by events
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(50):
+        ctx.render_device(cam, out.data_ptr(), 0, 6, args.precision, args.out, (0, 1), args.flags)
+    ev[1].record()
+    torch.cuda.synchronize()
+    res = {"label": f"{args.scene} flags={args.flags} out={args.out} sched={os.environ.get('RTC_SCHED_DIRECT', 'default')}",
+           "launch_us": round(ev[0].elapsed_time(ev[1]) * 1e3 / 50, 2),
            "workgroups": int(len(st)), "span_us": round(float(end.max()), 2),
            "start_q_us": q(start), "dur_q_us": q(dur), "end_q_us": q(end)}
     print(json.dumps(res))

@@ -1,10 +1,12 @@
 #!/bin/bash
+# Per-workgroup timelines (RT_FLAG_STAMPS) of the direct kernel on the
+# headline frame: full, camera-only (flags 4), camera-only with u8 output.
 set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd $R
-for s in grid static; do
-  for f in 0 1 5; do
-    RTC_SCHED_DIRECT=$s timeout -k 10 60 python scripts/stamps.py --flags $f 2>/dev/null | grep '^{'
-  done
+for args in "--flags 0" "--flags 4" "--flags 4 --out u8" "--flags 0 --out u8" "--flags 2"; do
+  timeout -k 10 60 python scripts/stamps.py $args 2>/dev/null | grep '^{' || exit 1
 done
-RTC_SCHED_POOL=dynamic timeout -k 10 60 python scripts/stamps.py --scene reflect_refract 2>/dev/null | grep '^{'
+for args in "--flags 0" "--flags 4"; do
+  RTC_SCHED_DIRECT=grid timeout -k 10 60 python scripts/stamps.py $args 2>/dev/null | grep '^{' || exit 1
+done
