@@ -626,8 +626,9 @@ int rt_context_create(int device_ordinal, rt_context** out) {
     RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreate(&ctx->ev_start));
     RT_HIP(hipEventCreate(&ctx->ev_stop));
-    RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_tile_counter), kTileQueues * sizeof(unsigned long long)));
-    RT_HIP(hipMemset(ctx->d_tile_counter, 0, kTileQueues * sizeof(unsigned long long)));
+    const size_t qbytes = (size_t)kTileQueues * kQueueStride * sizeof(unsigned long long);
+    RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_tile_counter), qbytes));
+    RT_HIP(hipMemset(ctx->d_tile_counter, 0, qbytes));
     const size_t counter_bytes = (size_t)kCounterShards * kNumCounters * sizeof(unsigned long long);
     RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_counters), counter_bytes));
     RT_HIP(hipMemset(ctx->d_counters, 0, counter_bytes));

@@ -37,6 +37,10 @@ constexpr int kCounterShards = 256;
 // pulls from queue b % 8 (blocks b and b+8 share an XCD under round-robin
 // dispatch; placement only affects speed).
 constexpr int kTileQueues = 8;
+// Queue heads sit kQueueStride u64 apart (256 B): adjacent heads shared one
+// cache line, so every XCD's dequeues serialized on it (~17 us per 1792
+// dequeues on MI355X).
+constexpr int kQueueStride = 32;
 // Tile scheduling modes (RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic)
 constexpr uint32_t kSchedGrid = 0;     // one workgroup per tile; the dispatcher balances
 constexpr uint32_t kSchedDynamic = 1;  // resident grid, per-XCD atomic tile queues
@@ -168,7 +172,7 @@ struct LaunchParams {
     uint32_t world_lds;      // bytes of world tables staged at the start of dynamic LDS (0 = none)
     void* spill;                 // pool overflow: grid x 8 x (pool_capacity - pool_lds_capacity) words
     unsigned long long* stamps;  // RT_FLAG_STAMPS: 2 x grid s_memrealtime values
-    unsigned long long* tile_counter;  // kTileQueues cumulative dequeue counters (one per XCD)
+    unsigned long long* tile_counter;  // kTileQueues cumulative dequeue counters, kQueueStride apart
     unsigned long long tile_base[kTileQueues];  // their values at this launch's start
     unsigned long long* counters;      // kCounterShards x kNumCounters cumulative u64
     int32_t* error_flag;               // set nonzero on pool overflow

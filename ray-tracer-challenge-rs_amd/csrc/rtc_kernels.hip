@@ -819,7 +819,7 @@ __device__ inline unsigned int next_tile(const LaunchParams<R>& P, uint32_t it, 
     }
     const uint32_t q = blockIdx.x % kTileQueues;
     if (it == 0 || pos == P.dequeue_chunk) {
-        chunk = atomicAdd(&P.tile_counter[q], 1ull) - P.tile_base[q];
+        chunk = atomicAdd(&P.tile_counter[q * kQueueStride], 1ull) - P.tile_base[q];
         pos = 0;
     }
     const unsigned long long t = q + (unsigned long long)kTileQueues * (chunk * P.dequeue_chunk + pos++);
@@ -882,6 +882,12 @@ __device__ inline DevScene<R> scene_view(const LaunchParams<R>& P, const ShapeRe
 // 8 (<= 64 VGPRs, spills at tile level) 48.9 us.
 #ifndef RTC_DIRECT_WAVES
 #define RTC_DIRECT_WAVES 7
+#endif
+// The f32 pool kernel sits at the 128-VGPR edge of 4 waves/SIMD (the 4
+// workgroups/CU its LDS pool is sized for): one register more drops it to 3
+// waves and costs ~60% (measured).  The cap keeps code changes off that cliff.
+#ifndef RTC_POOL_WAVES
+#define RTC_POOL_WAVES 4
 #endif
 template <typename R, bool kLds>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 4 ? RTC_DIRECT_WAVES : 1))) void trace_direct(
@@ -1015,7 +1021,8 @@ __device__ inline void acc_add(long long* acc, uint32_t pix, double v) {
 }
 
 template <typename R, bool kLds>
-__global__ __launch_bounds__(kBlock) void trace_pool(LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 4 ? RTC_POOL_WAVES : 1))) void trace_pool(
+    LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
     extern __shared__ __align__(16) unsigned char smem_all[];
     const DevScene<R> sc = scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem_all);
     if (P.stamps && threadIdx.x == 0) P.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
