@@ -55,7 +55,6 @@ struct DeviceWorld {
     PatternRec<R>* patterns = nullptr;
     LightRec<R>* lights = nullptr;
     int32_t* world_slot = nullptr;
-    std::vector<std::array<double, 4>> bounds;  // host copy of ShapeRec::bound per slot (f64)
     DevScene<R> scene{};
     void release() {
         (void)hipFree(world_slot);
@@ -94,7 +93,7 @@ struct rt_context {
     uint32_t sched_pool = rtc::kSchedDynamic;
     bool staged_store = false;  // RTC_STAGED_STORE=1 stages tile pixels in LDS
     bool lds_world = true;      // RTC_LDS_WORLD=0 gathers shade data from global memory
-    double cull_coverage = rtc::kCullMaxCoverage;  // RTC_CULL_COVERAGE (negative: no cull in the first kCullSlots)
+    bool cull = true;  // RTC_CULL=0 uploads every shape as unbounded (no wave cull; exactness tests)
     size_t occ_lds[8] = {};     // occupancy cache: {direct,pool} x {f32,f64} x {global,LDS world}
     int occ_blocks[8] = {};
     uint32_t direct_grid = 0;    // RTC_DIRECT_GRID: persistent grid size of the direct kernel (0 = resident)
@@ -180,41 +179,11 @@ void bounding_sphere(const rt_shape_desc& d, double out[4]) {
     out[3] = wr + pad;
 }
 
-// Per-launch cull mask: a bounded shape keeps its wave cull unless its
-// padded bounding sphere covers more than kCullMaxCoverage of the view
-// (estimated as the disc area pi tan^2(angular radius) over the image plane
-// area at unit distance, 4 half_width half_height).  Without a camera
-// (color_at rays) every bounded shape culls.
-uint64_t cull_mask(const std::vector<std::array<double, 4>>& bounds, const rt_camera_desc* cam, double max_coverage) {
-    uint64_t bits = 0;
-    if (max_coverage < 0.0) return 0;
-    const double view = cam ? 4.0 * cam->half_width * cam->half_height : 0.0;
-    for (size_t i = 0; i < bounds.size() && i < (size_t)kCullSlots; ++i) {
-        const auto& b = bounds[i];
-        if (!(b[3] >= 0.0)) continue;
-        bool cull = true;
-        if (cam && view > 0.0) {
-            const double v[3] = {b[0] - cam->origin[0], b[1] - cam->origin[1], b[2] - cam->origin[2]};
-            const double dist2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2], r2 = b[3] * b[3];
-            if (dist2 <= r2) {
-                cull = false;  // the camera is inside the bound
-            } else {
-                const double tan2 = r2 / (dist2 - r2);
-                cull = 3.14159265358979 * tan2 / view <= max_coverage;
-            }
-        }
-        if (cull) bits |= 1ull << i;
-    }
-    return bits;
-}
-
 template <typename R>
 int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes, uint32_t ns,
                 const rt_material_desc* mats, uint32_t nm, const rt_pattern_desc* pats, uint32_t np,
                 const rt_light_desc* lights, uint32_t nl) {
-    (void)ctx;
     w.release();
-    w.bounds.clear();
     std::vector<ShapeRec<R>> sh;
     std::vector<int32_t> begin(kNumKinds + 1, 0);
     for (int k = 0; k < kNumKinds; ++k) {
@@ -227,8 +196,7 @@ int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes,
             double bs[4];
             bounding_sphere(d, bs);
             for (int q = 0; q < 3; ++q) r.bound[q] = (R)bs[q];
-            r.bound[3] = bs[3] >= 0.0 ? (R)(bs[3] * bs[3]) : (R)-1;  // device keeps r^2
-            w.bounds.push_back({bs[0], bs[1], bs[2], bs[3]});
+            r.bound[3] = ctx->cull && bs[3] >= 0.0 ? (R)(bs[3] * bs[3]) : (R)-1;  // device keeps r^2
             r.ymin = (R)d.minimum;
             r.ymax = (R)d.maximum;
             for (int q = 0; q < 3; ++q) {
@@ -437,7 +405,6 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
            hipStream_t stream, uint32_t flags = 0) {
     LaunchParams<R> P{};
     P.scene = w.scene;
-    P.scene.cull_mask = cull_mask(w.bounds, cam, ctx->cull_coverage);
     if (cam) {
         for (int q = 0; q < 12; ++q) P.cam.inv[q] = (R)cam->inverse[q];
         for (int q = 0; q < 3; ++q) P.cam.origin[q] = (R)cam->origin[q];
@@ -620,7 +587,7 @@ int rt_context_create(int device_ordinal, rt_context** out) {
     ctx->sched_pool = sched(std::getenv("RTC_SCHED_POOL"), ctx->sched_pool);
     if (const char* e = std::getenv("RTC_STAGED_STORE")) ctx->staged_store = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_LDS_WORLD")) ctx->lds_world = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("RTC_CULL_COVERAGE")) ctx->cull_coverage = std::atof(e);
+    if (const char* e = std::getenv("RTC_CULL")) ctx->cull = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_POOL_LDS_RAYS")) ctx->pool_lds_rays = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("RTC_DIRECT_GRID")) ctx->direct_grid = (uint32_t)std::atoi(e);
     RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));

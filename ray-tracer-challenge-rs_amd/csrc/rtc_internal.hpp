@@ -50,12 +50,6 @@ constexpr int kDequeueChunkPool = 1;    // costly, high-variance tiles: balance 
 // World tables up to this size are staged into LDS for the per-lane gathers
 // (~120 f32 shapes); larger worlds gather from global memory (L2-resident).
 constexpr size_t kMaxWorldLds = 16 * 1024;
-// Wave cull (rtc_kernels.hip wave_may_hit) is decided per shape for the
-// first kCullSlots slots: a shape whose padded bounding sphere covers more
-// than kCullMaxCoverage of the camera's view is hit by most rays, so its
-// cull test would be pure overhead.
-constexpr int kCullSlots = 64;
-constexpr double kCullMaxCoverage = 1.0;
 
 // Fixed-point pixel accumulator of the pool kernel: contributions are summed
 // as int64 multiples of 2^-48 so the per-pixel sum is independent of the
@@ -137,11 +131,6 @@ struct DevScene {
     const PatternRec<R>* lpats;
     const int32_t* lworld_slot;
     int32_t kind_begin[kNumKinds + 1];
-    // Per-launch: slot s < kCullSlots runs the wave cull iff bit s is set
-    // (slots past kCullSlots always do).  Set by the host from the camera.
-    // One 64-bit mask: a shift and an AND in SGPRs per shape test (an array
-    // needed a compare/select chain, ~16 SALU per test).
-    uint64_t cull_mask;
     int32_t n_materials, n_patterns;
     int32_t n_lights;
     int32_t any_secondary;  // some material has reflectiveness or transparency != 0

@@ -377,14 +377,13 @@ __device__ inline void for_all_kinds(const DevScene<R>& sc, F&& f) {
 __device__ inline bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 
 template <typename R>
-__device__ inline bool wave_may_hit(const DevScene<R>& sc, const ShapeRec<R>& s, int slot, V3<R> o, V3<R> d) {
+__device__ inline bool wave_may_hit(const ShapeRec<R>& s, V3<R> o, V3<R> d) {
     const R r2 = s.bound[3];  // radius^2
     if (!(r2 >= (R)0)) return true;  // unbounded shape: wave-uniform
-    if (slot < kCullSlots && !((sc.cull_mask >> slot) & 1ull)) return true;
     const V3<R> oc = {s.bound[0] - o.x, s.bound[1] - o.y, s.bound[2] - o.z};
     // |d x oc|^2 = |oc|^2 |d|^2 - (oc.d)^2 (Lagrange): reuses oc.d of the
     // front test.  Rounding of the two products is bounded by ~12 ulp of
-    // |oc|^2 |d|^2; shrinking |oc|^2 by kCullSlack (>> that) keeps the test
+    // |oc|^2 |d|^2; shrinking |oc|^2 by 1 - kKeep (>> that) keeps the test
     // conservative, so no lane that meets the sphere is ever rejected.
     constexpr R kKeep = sizeof(R) == 4 ? (R)(1 - 1e-5) : (R)(1 - 1e-12);
     const R tc = dot(oc, d), oo = dot(oc, oc);
@@ -411,7 +410,7 @@ __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
     R ht = Real<R>::kInf;
     int hw = INT_MAX;
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
-        if (!wave_may_hit(sc, s, slot, o, d)) return;
+        if (!wave_may_hit(s, o, d)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
         const int w = s.world_index;
@@ -437,7 +436,7 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) 
     bool hit = false;
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
         if (!s.casts_shadow) return;  // wave-uniform
-        if (!wave_may_hit(sc, s, slot, o, d)) return;
+        if (!wave_may_hit(s, o, d)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
         entries<R, K>(s, lo, ld, [&](R t, bool v) { hit |= v & (t >= (R)0) & (t < dist); });

@@ -191,16 +191,15 @@ def _render_with_env(rtc, monkeypatch, env, scene, cam, precision):
 @pytest.mark.parametrize("name", ["three_sphere_scene", "shadow_puppets", "cover", "table", "cylinders", "metal"])
 def test_cull_is_exact(gpu_ctx, rtc, monkeypatch, name, precision):
     """The wave cull is acceleration only: the frame with the cull off
-    (RTC_CULL_COVERAGE=-1) and forced on for every bounded shape (1e30)
-    equals the default frame bit for bit, counters included."""
+    (RTC_CULL=0: every shape uploaded as unbounded) equals the default frame
+    bit for bit, counters included."""
     scene = scene_fixture(name)
     cam = rtc.camera_resize(scene.camera, 320, 200)
     gpu_ctx.upload(scene)
     a, sa = gpu_ctx.render(cam, 6, precision=precision)
-    for cov in ("-1", "1e30"):
-        b, sb = _render_with_env(rtc, monkeypatch, {"RTC_CULL_COVERAGE": cov}, scene, cam, precision)
-        assert np.array_equal(a, b), f"{name} {precision}: cull<={cov} changed {int((a != b).any(axis=2).sum())} px"
-        assert _counts(sa) == _counts(sb)
+    b, sb = _render_with_env(rtc, monkeypatch, {"RTC_CULL": "0"}, scene, cam, precision)
+    assert np.array_equal(a, b), f"{name} {precision}: the cull changed {int((a != b).any(axis=2).sum())} px"
+    assert _counts(sa) == _counts(sb)
 
 
 @pytest.mark.parametrize("precision", ["f32", "f64"])
@@ -228,7 +227,7 @@ def test_cull_is_exact_for_grazing_rays(gpu_ctx, rtc, monkeypatch, precision):
     rays = np.concatenate([o, d], axis=1)
     gpu_ctx.upload(tables)
     a, sa = gpu_ctx.color_at(rays, precision=precision)
-    monkeypatch.setenv("RTC_CULL_COVERAGE", "-1")
+    monkeypatch.setenv("RTC_CULL", "0")
     with rtc.Context(0) as c:
         c.upload(tables)
         b, sb = c.color_at(rays, precision=precision)
