@@ -580,27 +580,51 @@ __device__ inline V3<R> pattern_color(const DevScene<R>& sc, int pid, const Shap
 }
 
 // Per-thread event counters (rt_stats order).
+// Event counters of one wave (rt_stats order), kept wave-uniform: each
+// event is counted as popcount(ballot(flag)) at a point every lane of the
+// wave reaches, so the counters live in SGPRs (per-lane counters cost 8
+// VGPRs, a v_add per event and a 48-shuffle reduction per wave).
 struct Counts {
     uint32_t c[kNumCounters];
 };
+
+__device__ inline uint32_t wave_count(bool p) {
+    return (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(p));
+}
 
 // One radiance ray: closest hit, shading over all lights with shadow rays,
 // and the (at most two) children.  Returns false on a miss.
 template <typename R>
 struct Shaded {
     V3<R> surface;  // Σ_lights lighting(...)  (world.rs:44-52)
-    bool refl_child, refr_child;
+    bool refl_child = false, refr_child = false;
+    bool patterned = false;  // each light evaluation samples a pattern
+    bool refr_eval = false;  // refracted_color past the opaque/depth check
+    bool schlick = false;    // schlicks_approximation evaluated
     V3<R> refl_o, refl_d, refr_o, refr_d;
     R refl_w, refr_w;  // reflectiveness × {R | 1}, transparency × {1-R | 1}
 };
 
+// Count one wave's events after shading (call where every lane arrives):
+// `primary` rays entering the path, `hit` = shade_ray's result.
+template <typename R>
+__device__ inline void count_events(Counts& k, bool primary, bool hit, const Shaded<R>& sh, int n_lights) {
+    k.c[0] += wave_count(primary);
+    const uint32_t shaded = wave_count(hit);
+    k.c[4] += shaded;
+    k.c[1] += shaded * (uint32_t)n_lights;  // world.rs:46-52: one shadow ray per light
+    k.c[5] += wave_count(hit & sh.patterned) * (uint32_t)n_lights;
+    k.c[2] += wave_count(hit & sh.refl_child);
+    k.c[3] += wave_count(hit & sh.refr_child);
+    k.c[6] += wave_count(hit & sh.refr_eval);
+    k.c[7] += wave_count(hit & sh.schlick);
+}
+
 template <typename R, bool kChildren>
-__device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32_t remaining, Shaded<R>& out,
-                                 Counts& k) {
+__device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32_t remaining, Shaded<R>& out) {
     using T = Real<R>;
     const Hit<R> h = closest_hit(sc, o, d);
     if (h.slot < 0) return false;  // world.rs:85: miss -> BLACK
-    k.c[4]++;                      // shaded
     const ShapeRec<R>& s = sc.lshapes[h.slot];
     // prepare_computations, intersection.rs:21-31
     const V3<R> p = along(o, d, h.t);
@@ -612,6 +636,7 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
     // material.rs:75-80: the pattern is sampled at over_point, once per hit
     V3<R> base = {m.color[0], m.color[1], m.color[2]};
     const bool patterned = m.pattern >= 0;
+    out.patterned = patterned;
     if (patterned) base = pattern_color(sc, m.pattern, s, over);
     V3<R> surface = {(R)0, (R)0, (R)0};
     for (int li = 0; li < sc.n_lights; ++li) {
@@ -621,8 +646,6 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
         const R dist = magnitude(to_light);
         const V3<R> ld = normalized(to_light);  // == to_light / dist (world.rs:104-106)
         const bool shadowed = any_hit(sc, over, ld, dist);
-        k.c[1]++;
-        if (patterned) k.c[5]++;
         // calculate_lighting, material.rs:83-114
         const V3<R> eff = {base.x * L.intensity[0], base.y * L.intensity[1], base.z * L.intensity[2]};
         V3<R> c = {eff.x * m.ambient, eff.y * m.ambient, eff.z * m.ambient};
@@ -643,17 +666,15 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
     }
     out.surface = surface;
     out.refl_child = out.refr_child = false;
-    if constexpr (!kChildren) {
-        // shade_hit evaluates Schlick whenever the material is both (world.rs:59-60)
-        if (m.reflectiveness > (R)0 && m.transparency > (R)0) k.c[7]++;
-    } else {
+    // shade_hit evaluates Schlick whenever the material is both (world.rs:59-60)
+    out.schlick = (m.reflectiveness > (R)0) & (m.transparency > (R)0);
+    if constexpr (kChildren) {
         const bool reflective = m.reflectiveness > (R)0, transparent = m.transparency > (R)0;
         R n1 = (R)1, n2 = (R)1;
         if (m.transparency != (R)0) refractive_indices(sc, o, d, h, n1, n2);
         // Schlick mixing only when both (world.rs:59-66)
         R fr = (R)1, ft = (R)1;
         if (reflective && transparent) {  // computed_hit.rs:50-68
-            k.c[7]++;
             R cs = dot(eye, n);
             bool total = false;
             if (n1 > n2) {
@@ -677,10 +698,9 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
             out.refl_o = over;
             out.refl_d = reflect(d, n);
             out.refl_w = m.reflectiveness * fr;
-            k.c[2]++;
         }
         if (remaining > 0 && m.transparency != (R)0) {  // world.rs:130-157
-            k.c[6]++;
+            out.refr_eval = true;
             const R nr = T::div(n1, n2);
             const R cos_i = dot(eye, n);
             const R sin2_t = (nr * nr) * ((R)1 - cos_i * cos_i);
@@ -691,7 +711,6 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
                 out.refr_o = along(p, n, -T::kOffset);  // under_point, computed_hit.rs:34
                 out.refr_d = {n.x * f - eye.x * nr, n.y * f - eye.y * nr, n.z * f - eye.z * nr};
                 out.refr_w = m.transparency * ft;
-                k.c[3]++;
             }
         }
     }
@@ -769,15 +788,12 @@ __device__ inline void load_primary(const LaunchParams<R>& P, uint32_t t, uint32
     }
 }
 
-// Wave reduction of the event counters, then lane 0 adds them into the wave's
-// counter shard (no LDS, no barrier).
+// Lane 0 adds the wave's (uniform) counters into the wave's counter shard.
 __device__ inline void flush_counts(const Counts& k, unsigned long long* global) {
     const uint32_t shard = (blockIdx.x * (kBlock / 64) + threadIdx.x / 64) % kCounterShards;
-    for (int i = 0; i < kNumCounters; ++i) {
-        unsigned int v = k.c[i];
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&global[shard * kNumCounters + i], (unsigned long long)v);
-    }
+    if ((threadIdx.x & 63) == 0)
+        for (int i = 0; i < kNumCounters; ++i)
+            if (k.c[i]) atomicAdd(&global[shard * kNumCounters + i], (unsigned long long)k.c[i]);
 }
 
 // Write one tile of RT_OUT_REAL pixels: colours are staged in LDS in the
@@ -882,11 +898,15 @@ __device__ inline DevScene<R> scene_view(const LaunchParams<R>& P, const ShapeRe
 #ifndef RTC_DIRECT_WAVES
 #define RTC_DIRECT_WAVES 7
 #endif
-// The f32 pool kernel sits at the 128-VGPR edge of 4 waves/SIMD (the 4
-// workgroups/CU its LDS pool is sized for): one register more drops it to 3
-// waves and costs ~60% (measured).  The cap keeps code changes off that cliff.
+// Waves per SIMD of the f32 pool kernel (VGPRs <= 512 / waves; its LDS pool
+// is sized to match, rtc_host.cpp pool_lds_rays).  Occupancy beats spills
+// here: same-box A/B (scripts/ab_builds.sh), kernel time vs 4 waves (111
+// VGPRs): 6 waves (80 VGPRs, 108 B/lane scratch) cover -11%, metal -7%,
+// reflect_refract/table/refraction -4..-6%, cylinders +4%; 7 and 8 waves
+// spill more and lose.  Without a cap a code change that crosses 128 VGPRs
+// drops to 3 waves (~60% slower, measured).
 #ifndef RTC_POOL_WAVES
-#define RTC_POOL_WAVES 4
+#define RTC_POOL_WAVES 6
 #endif
 template <typename R, bool kLds>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 4 ? RTC_DIRECT_WAVES : 1))) void trace_direct(
@@ -909,9 +929,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         uint64_t out_idx;
         load_primary(P, t, tid, valid, o, d, out_idx);
         V3<R> c = {(R)0, (R)0, (R)0};
+        Shaded<R> sh;
+        bool hit = false;
         if (valid) {
-            k.c[0]++;
-            Shaded<R> sh;
             if (P.flags & (RT_FLAG_NO_SHADE | RT_FLAG_NO_TRACE)) {
                 if (P.flags & RT_FLAG_NO_TRACE) {
                     c = d;
@@ -919,10 +939,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
                     const Hit<R> h = closest_hit(sc, o, d);
                     c = {h.t * (R)0.01, (R)h.slot, (R)0};
                 }
-            } else if (shade_ray<R, false>(sc, o, d, 0, sh, k)) {
+            } else if (shade_ray<R, false>(sc, o, d, 0, sh)) {
+                hit = true;
                 c = sh.surface;
             }
         }
+        count_events(k, valid, hit, sh, sc.n_lights);
         if (staged)
             store_tile(P, t, c, s_px);
         else if (valid)
@@ -1056,7 +1078,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         V3<R> o, d;
         uint64_t out_idx;
         load_primary(P, t, tid, valid, o, d, out_idx);
-        if (valid) k.c[0]++;
+        k.c[0] += wave_count(valid);
         {
             const int slot = wave_reserve(valid, &s_top[0]);
             if (valid) pool_put(pl, slot, o, d, (R)1, tid | (P.max_depth << 8));
@@ -1077,7 +1099,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
             __syncthreads();  // every lane holds its ray; the next top is set
             Shaded<R> sh;
             bool hit = false;
-            if (active) hit = shade_ray<R, true>(sc, ro, rd, meta >> 8, sh, k);
+            if (active) hit = shade_ray<R, true>(sc, ro, rd, meta >> 8, sh);
+            count_events(k, false, hit, sh, sc.n_lights);
             const uint32_t pix = meta & 0xFFu;
             if (hit) {
                 acc_add(pl.acc, pix, (double)(sh.surface.x * rw));

@@ -10,7 +10,7 @@ VARIANTS=${1:-default}
 SCENES=${2:-three_sphere_scene}
 shift 2 || true
 ENVS=("${@:-X=0}")
-B="python bench.py --steps 300 --warmup 20 --no-cpu-baseline"
+B="python bench.py --steps ${AB_STEPS:-1000} --warmup 30 --no-cpu-baseline"
 for sc in $SCENES; do
   for v in $VARIANTS; do
     lib=$R/ray-tracer-challenge-rs_amd/rtc_amd/_lib/librtc.so
