@@ -28,6 +28,8 @@ template <typename R>
 hipError_t launch_trace(const LaunchParams<R>& P, bool pool, uint32_t grid, size_t dyn_lds, hipStream_t stream);
 template <typename R>
 hipError_t occupancy(bool pool, bool lds, size_t dyn_lds, int* blocks_per_cu);
+template <typename R>
+hipError_t static_lds(bool pool, bool lds, size_t* bytes);
 hipError_t launch_assemble(const void* gathered, void* image, uint32_t width, uint32_t height, uint32_t shards,
                            uint32_t strip_rows, uint32_t bpp, hipStream_t stream);
 
@@ -78,7 +80,6 @@ struct rt_context {
     hipStream_t stream = nullptr;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     unsigned long long* d_tile_counter = nullptr;
-    unsigned long long tile_base[rtc::kTileQueues] = {};
     unsigned long long* d_counters = nullptr;  // kNumCounters cumulative
     int32_t* d_error = nullptr;
     bool have_scene = false;
@@ -91,7 +92,6 @@ struct rt_context {
     // staging barriers wait for store completion).
     uint32_t sched_direct = rtc::kSchedStatic;  // RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic
     uint32_t sched_pool = rtc::kSchedDynamic;
-    bool staged_store = false;  // RTC_STAGED_STORE=1 stages tile pixels in LDS
     bool lds_world = true;      // RTC_LDS_WORLD=0 gathers shade data from global memory
     bool cull = true;  // RTC_CULL=0 uploads every shape as unbounded (no wave cull; exactness tests)
     size_t occ_lds[8] = {};     // occupancy cache: {direct,pool} x {f32,f64} x {global,LDS world}
@@ -307,7 +307,8 @@ size_t pool_lds_bytes(uint32_t cap) {
     return 3 * kBlock * sizeof(long long) + (size_t)cap * (7 * sizeof(R) + sizeof(uint32_t));
 }
 
-constexpr size_t kMaxLds = 160 * 1024 - 8 * 1024;  // leave room for static LDS (tile staging)
+constexpr size_t kLdsPerCu = 160 * 1024;
+constexpr size_t kMaxLds = kLdsPerCu - 8 * 1024;  // dynamic LDS of one workgroup (room for static)
 
 struct LaunchShape {
     bool pool;
@@ -319,7 +320,8 @@ struct LaunchShape {
 };
 
 // Cached occupancy (workgroups per CU) of one kernel instantiation at a
-// given dynamic LDS size.
+// given dynamic LDS size: the occupancy API's register/wave limit, and the
+// LDS limit computed here from static + dynamic bytes (512-byte granules).
 template <typename R>
 int blocks_per_cu(rt_context* ctx, bool pool, bool lds_world, size_t lds, int* per_cu) {
     const int key = (pool ? 1 : 0) + (sizeof(R) == 8 ? 2 : 0) + (lds_world ? 4 : 0);
@@ -327,7 +329,13 @@ int blocks_per_cu(rt_context* ctx, bool pool, bool lds_world, size_t lds, int* p
         *per_cu = ctx->occ_blocks[key];
         return RT_OK;
     }
-    RT_HIP(occupancy<R>(pool, lds_world, lds, per_cu));
+    int api = 0;
+    size_t st = 0;
+    RT_HIP(occupancy<R>(pool, lds_world, lds, &api));
+    RT_HIP(static_lds<R>(pool, lds_world, &st));
+    const size_t per_block = (st + lds + 511) / 512 * 512;
+    const int by_lds = per_block ? (int)((size_t)kLdsPerCu / per_block) : api;
+    *per_cu = std::min(api, by_lds);
     ctx->occ_lds[key] = lds;
     ctx->occ_blocks[key] = *per_cu;
     return RT_OK;
@@ -348,11 +356,13 @@ int pool_lds_rays(rt_context* ctx, uint32_t world_lds, uint32_t cap, uint32_t* l
     if ((rc = blocks_per_cu<R>(ctx, true, lw, world_lds + pool_lds_bytes<R>(kBlock), &best))) return rc;
     if (best < 1) best = 1;
     const size_t rec = 7 * sizeof(R) + sizeof(uint32_t);
-    const size_t budget = 160 * 1024 / (size_t)best;
-    const size_t fixed = world_lds + pool_lds_bytes<R>(0);
+    const size_t budget = (size_t)kLdsPerCu / (size_t)best;
+    size_t st = 0;
+    RT_HIP(static_lds<R>(true, lw, &st));
+    const size_t fixed = st + world_lds + pool_lds_bytes<R>(0) + 511;
     uint32_t n = budget > fixed ? (uint32_t)((budget - fixed) / rec) : kBlock;
     n = std::min<uint32_t>(cap, std::max<uint32_t>(kBlock, n & ~31u));
-    for (;;) {  // static LDS (tile staging) is not in `fixed`: step down until it fits
+    for (;;) {  // granule rounding: step down until `best` workgroups fit
         int got = 0;
         if ((rc = blocks_per_cu<R>(ctx, true, lw, world_lds + pool_lds_bytes<R>(n), &got))) return rc;
         if (got >= best || n <= (uint32_t)kBlock) break;
@@ -448,22 +458,14 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
         P.spill = ctx->d_spill;
     }
     P.persistent = ls.sched;
-    P.dequeue_chunk = ls.pool ? kDequeueChunkPool : kDequeueChunkDirect;
-    P.staged_store = ctx->staged_store ? 1 : 0;
     P.flags = flags;
     P.world_lds = ls.world_lds;
-    // Queue q holds tiles q, q+8, ... and serves workgroups q, q+8, ....  The
-    // atomics one launch makes on queue q: one per chunk handed out, plus one
-    // failing fetch per workgroup — except the workgroup that ends inside a
-    // partial last chunk, which stops without fetching again.
-    for (int q = 0; q < kTileQueues && ls.sched == kSchedDynamic; ++q) {
-        P.tile_base[q] = ctx->tile_base[q];
-        const uint64_t C = P.dequeue_chunk;
-        const uint64_t tiles_q = P.n_tiles > (uint32_t)q ? (P.n_tiles - q + kTileQueues - 1) / kTileQueues : 0;
-        const uint64_t chunks_q = (tiles_q + C - 1) / C;
-        const uint64_t blocks_q = ls.grid > (uint32_t)q ? (ls.grid - q + kTileQueues - 1) / kTileQueues : 0;
-        const uint64_t partial_q = (tiles_q % C) != 0 ? 1 : 0;
-        ctx->tile_base[q] += chunks_q + blocks_q - partial_q;
+    // Dynamic launches start from zeroed queue heads (stream-ordered; the
+    // workgroups' stealing makes a launch's atomic count data-dependent).
+    if (ls.sched == kSchedDynamic) {
+        P.tile_counter = ctx->d_tile_counter;
+        RT_HIP(hipMemsetAsync(ctx->d_tile_counter, 0,
+                              (size_t)kTileQueues * kQueueStride * sizeof(unsigned long long), stream));
     }
     if (flags & RT_FLAG_STAMPS) {
         if (ctx->stamp_capacity < ls.grid) {
@@ -585,7 +587,6 @@ int rt_context_create(int device_ordinal, rt_context** out) {
     };
     ctx->sched_direct = sched(std::getenv("RTC_SCHED_DIRECT"), ctx->sched_direct);
     ctx->sched_pool = sched(std::getenv("RTC_SCHED_POOL"), ctx->sched_pool);
-    if (const char* e = std::getenv("RTC_STAGED_STORE")) ctx->staged_store = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_LDS_WORLD")) ctx->lds_world = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_CULL")) ctx->cull = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_POOL_LDS_RAYS")) ctx->pool_lds_rays = (uint32_t)std::atoi(e);

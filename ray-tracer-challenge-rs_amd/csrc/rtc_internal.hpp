@@ -45,8 +45,6 @@ constexpr int kQueueStride = 32;
 constexpr uint32_t kSchedGrid = 0;     // one workgroup per tile; the dispatcher balances
 constexpr uint32_t kSchedDynamic = 1;  // resident grid, per-XCD atomic tile queues
 constexpr uint32_t kSchedStatic = 2;   // resident grid, tiles b, b+G, ... (no atomics)
-constexpr int kDequeueChunkDirect = 4;  // tiles per dequeue: cheap, uniform tiles
-constexpr int kDequeueChunkPool = 1;    // costly, high-variance tiles: balance first
 // World tables up to this size are staged into LDS for the per-lane gathers
 // (~120 f32 shapes); larger worlds gather from global memory (L2-resident).
 constexpr size_t kMaxWorldLds = 16 * 1024;
@@ -155,14 +153,11 @@ struct LaunchParams {
     uint32_t pool_lds_capacity;  // of which held in LDS; the rest in `spill`
     uint32_t pop_batch;      // pool kernel: rays popped per iteration (<= kBlock)
     uint32_t persistent;     // kSched*: tile scheduling of this launch
-    uint32_t dequeue_chunk;  // tiles per dequeue (persistent mode)
-    uint32_t staged_store;   // stage tile pixels in LDS for contiguous stores
     uint32_t flags;          // RT_FLAG_* diagnostic ablations
     uint32_t world_lds;      // bytes of world tables staged at the start of dynamic LDS (0 = none)
     void* spill;                 // pool overflow: grid x 8 x (pool_capacity - pool_lds_capacity) words
     unsigned long long* stamps;  // RT_FLAG_STAMPS: 2 x grid s_memrealtime values
-    unsigned long long* tile_counter;  // kTileQueues cumulative dequeue counters, kQueueStride apart
-    unsigned long long tile_base[kTileQueues];  // their values at this launch's start
+    unsigned long long* tile_counter;  // kTileQueues queue heads, kQueueStride apart, zeroed per launch
     unsigned long long* counters;      // kCounterShards x kNumCounters cumulative u64
     int32_t* error_flag;               // set nonzero on pool overflow
 };

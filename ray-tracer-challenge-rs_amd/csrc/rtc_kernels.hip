@@ -796,49 +796,29 @@ __device__ inline void flush_counts(const Counts& k, unsigned long long* global)
             if (k.c[i]) atomicAdd(&global[shard * kNumCounters + i], (unsigned long long)k.c[i]);
 }
 
-// Write one tile of RT_OUT_REAL pixels: colours are staged in LDS in the
-// output's row-major order and written back one element per lane, so each
-// wave-wide store covers 64 consecutive elements (256 B for f32) instead of
-// three 12-byte-strided partial lines per pixel.  Canvas edges are masked.
+// Next tile of this workgroup (called by thread 0 only; `probe` lives in
+// its registers).  kSchedGrid: one workgroup per tile; kSchedStatic: tiles
+// b, b+G, b+2G, ... of a resident grid, no atomics; kSchedDynamic: per-XCD
+// queues, queue q holding tiles q, q+8, ....  A workgroup drains queue
+// b % 8 (its XCD's under round-robin dispatch) and then steals from the
+// others in turn: without stealing, a queue whose tiles were cheap left its
+// XCD idle while another XCD's queue ran 300-450 us longer (reflect_refract,
+// per-workgroup timestamps).  The heads are zeroed before every launch that
+// uses them (a stream-ordered memset), so their atomics need no bookkeeping.
 template <typename R>
-__device__ inline void store_tile(const LaunchParams<R>& P, uint32_t t, V3<R> c, R* s_px) {
-    const uint32_t tid = threadIdx.x;
-    s_px[3 * tid + 0] = c.x;
-    s_px[3 * tid + 1] = c.y;
-    s_px[3 * tid + 2] = c.z;
-    __syncthreads();
-    const uint32_t lrow = t / P.tiles_x, tcol = t - lrow * P.tiles_x;
-    const uint32_t x0 = tcol * RT_TILE_W, y0 = (lrow * P.shard_count + P.shard_index) * RT_TILE_H;
-    const uint32_t ncols = min((uint32_t)RT_TILE_W, P.width - x0);
-    const uint32_t nrows = y0 < P.height ? min((uint32_t)RT_TILE_H, P.height - y0) : 0u;
-    constexpr uint32_t kRowElems = 3 * RT_TILE_W;
-    R* out = static_cast<R*>(P.out) + ((uint64_t)lrow * RT_TILE_H * P.width + x0) * 3;
-    for (uint32_t i = tid; i < RT_TILE_H * kRowElems; i += kBlock) {
-        const uint32_t row = i / kRowElems, e = i - row * kRowElems;
-        if (row < nrows && e < 3 * ncols) out[(uint64_t)row * P.width * 3 + e] = s_px[i];
-    }
-    __syncthreads();  // s_px is reused by the next tile
-}
-
-// Next tile of this workgroup (called by thread 0 only; `chunk`/`pos` live in
-// its registers).  Persistent mode pulls kDequeueChunk consecutive tiles of
-// its queue (see kTileQueues) per returning atomic, so the ~1-3 us atomic
-// round trip is paid once per chunk, not per tile.
-template <typename R>
-__device__ inline unsigned int next_tile(const LaunchParams<R>& P, uint32_t it, unsigned long long& chunk,
-                                         uint32_t& pos) {
-    if (P.persistent == kSchedGrid) return it == 0 ? blockIdx.x : 0xFFFFFFFFu;  // one workgroup per tile
-    if (P.persistent == kSchedStatic) {  // resident grid, tiles b, b+G, b+2G, ... (no atomics)
+__device__ inline unsigned int next_tile(const LaunchParams<R>& P, uint32_t it, uint32_t& probe) {
+    if (P.persistent == kSchedGrid) return it == 0 ? blockIdx.x : 0xFFFFFFFFu;
+    if (P.persistent == kSchedStatic) {
         const unsigned long long t = blockIdx.x + (unsigned long long)it * gridDim.x;
         return t < P.n_tiles ? (unsigned int)t : 0xFFFFFFFFu;
     }
-    const uint32_t q = blockIdx.x % kTileQueues;
-    if (it == 0 || pos == P.dequeue_chunk) {
-        chunk = atomicAdd(&P.tile_counter[q * kQueueStride], 1ull) - P.tile_base[q];
-        pos = 0;
+    for (; probe < (uint32_t)kTileQueues; ++probe) {
+        const uint32_t q = (blockIdx.x + probe) % kTileQueues;
+        const unsigned long long j = atomicAdd(&P.tile_counter[q * kQueueStride], 1ull);
+        const unsigned long long t = q + (unsigned long long)kTileQueues * j;
+        if (t < P.n_tiles) return (unsigned int)t;
     }
-    const unsigned long long t = q + (unsigned long long)kTileQueues * (chunk * P.dequeue_chunk + pos++);
-    return t < P.n_tiles ? (unsigned int)t : 0xFFFFFFFFu;
+    return 0xFFFFFFFFu;
 }
 
 // The world as seen by one launch, rebuilt from the restrict parameters.
@@ -914,10 +894,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     extern __shared__ __align__(16) unsigned char smem[];
     const DevScene<R> sc = scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem);
     if (P.stamps && threadIdx.x == 0) P.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-    __shared__ R s_px[3 * kBlock];
     Counts k = {};
     const uint32_t tid = threadIdx.x;
-    const bool staged = P.staged_store && !P.rays && P.out_format == RT_OUT_REAL;
     // Tiles b, b+G, b+2G, ...: with G = n_tiles (kSchedGrid) one tile per
     // workgroup, with G = resident workgroups (kSchedStatic) a persistent
     // grid.  Primary-only tiles cost the same, so no queue is needed, and the
@@ -945,10 +923,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
             }
         }
         count_events(k, valid, hit, sh, sc.n_lights);
-        if (staged)
-            store_tile(P, t, c, s_px);
-        else if (valid)
-            store_pixel(P, out_idx, c);
+        if (valid) store_pixel(P, out_idx, c);
     }
     if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
     if (P.stamps) {
@@ -1050,7 +1025,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     unsigned char* smem = smem_all + (kLds ? P.world_lds : 0);
     __shared__ unsigned int s_tile[2];
     __shared__ int s_top[2];
-    __shared__ R s_px[3 * kBlock];
     const uint32_t cap = P.pool_capacity;
     const uint32_t lcap = P.pool_lds_capacity, gcap = cap - lcap;
     Pool<R> pl;
@@ -1063,11 +1037,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
 
     Counts k = {};
     const uint32_t tid = threadIdx.x;
-    unsigned long long chunk = 0;
-    uint32_t pos = 0;
+    uint32_t probe = 0;
     for (uint32_t it = 0;; ++it) {
         if (tid == 0) {
-            s_tile[it & 1] = next_tile(P, it, chunk, pos);
+            s_tile[it & 1] = next_tile(P, it, probe);
             s_top[0] = 0;
         }
         for (int c = 0; c < 3; ++c) pl.acc[c * kBlock + tid] = 0;
@@ -1128,10 +1101,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         }
         const V3<R> c = {(R)((double)pl.acc[tid] * kAccInvScale), (R)((double)pl.acc[kBlock + tid] * kAccInvScale),
                          (R)((double)pl.acc[2 * kBlock + tid] * kAccInvScale)};
-        if (P.staged_store && !P.rays && P.out_format == RT_OUT_REAL)
-            store_tile(P, t, c, s_px);
-        else if (valid)
-            store_pixel(P, out_idx, c);
+        if (valid) store_pixel(P, out_idx, c);
         __syncthreads();  // accumulators are re-zeroed for the next tile
     }
     if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
@@ -1184,6 +1154,24 @@ hipError_t occupancy(bool pool, bool lds, size_t dyn_lds, int* blocks_per_cu) {
                : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_direct<R, false>, kBlock, dyn_lds);
 }
 
+// Static LDS of one instantiation (the occupancy API's LDS accounting
+// proved optimistic: it promised 6 pool workgroups/CU where 5 fit).
+template <typename R>
+hipError_t static_lds(bool pool, bool lds, size_t* bytes) {
+    hipFuncAttributes a{};
+    hipError_t e;
+    if (pool)
+        e = lds ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(trace_pool<R, true>))
+                : hipFuncGetAttributes(&a, reinterpret_cast<const void*>(trace_pool<R, false>));
+    else
+        e = lds ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(trace_direct<R, true>))
+                : hipFuncGetAttributes(&a, reinterpret_cast<const void*>(trace_direct<R, false>));
+    *bytes = a.sharedSizeBytes;
+    return e;
+}
+
+template hipError_t static_lds<float>(bool, bool, size_t*);
+template hipError_t static_lds<double>(bool, bool, size_t*);
 template hipError_t launch_trace<float>(const LaunchParams<float>&, bool, uint32_t, size_t, hipStream_t);
 template hipError_t launch_trace<double>(const LaunchParams<double>&, bool, uint32_t, size_t, hipStream_t);
 template hipError_t occupancy<float>(bool, bool, size_t, int*);

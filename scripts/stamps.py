@@ -55,6 +55,12 @@ def main():
            "launch_us": round(ev[0].elapsed_time(ev[1]) * 1e3 / 50, 2),
            "workgroups": int(len(st)), "span_us": round(float(end.max()), 2),
            "start_q_us": q(start), "dur_q_us": q(dur), "end_q_us": q(end)}
+    if os.environ.get("STAMPS_DETAIL"):
+        late = np.where(start > 5.0)[0]
+        res["late_starters"] = int(len(late))
+        res["late_by_queue"] = np.bincount(late % 8, minlength=8).tolist()
+        res["end_max_by_queue_us"] = [round(float(end[np.arange(len(end)) % 8 == q].max()), 1) for q in range(8)]
+        res["end_med_by_queue_us"] = [round(float(np.median(end[np.arange(len(end)) % 8 == q])), 1) for q in range(8)]
     print(json.dumps(res))
     ctx.close()
 
