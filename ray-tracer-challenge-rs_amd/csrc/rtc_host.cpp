@@ -28,8 +28,8 @@ template <typename R>
 hipError_t launch_trace(const LaunchParams<R>& P, bool pool, uint32_t grid, size_t dyn_lds, hipStream_t stream);
 template <typename R>
 hipError_t occupancy(bool pool, bool lds, size_t dyn_lds, int* blocks_per_cu);
-template <typename R>
-hipError_t static_lds(bool pool, bool lds, size_t* bytes);
+
+hipError_t launch_order_tiles(const uint32_t* cost, uint32_t* order, uint32_t n, hipStream_t stream);
 hipError_t launch_assemble(const void* gathered, void* image, uint32_t width, uint32_t height, uint32_t shards,
                            uint32_t strip_rows, uint32_t bpp, hipStream_t stream);
 
@@ -77,6 +77,7 @@ struct DeviceWorld {
 struct rt_context {
     int device = 0;
     int cu_count = 0;
+    size_t lds_per_block = 64 * 1024;
     hipStream_t stream = nullptr;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     unsigned long long* d_tile_counter = nullptr;
@@ -99,6 +100,15 @@ struct rt_context {
     uint32_t direct_grid = 0;    // RTC_DIRECT_GRID: persistent grid size of the direct kernel (0 = resident)
     uint32_t pool_lds_rays = 0;  // RTC_POOL_LDS_RAYS: LDS-resident pool slots (0 = sized for occupancy)
     void* d_spill = nullptr;     // ray-pool overflow regions, one per resident workgroup
+    // Heaviest-first tile order for repeated pool launches of the same frame
+    // (order_tiles): per-tile costs of the last launch and its signature.
+    bool tile_order = true;      // RTC_TILE_ORDER=0: raster order always
+    uint32_t* d_tile_cost = nullptr;
+    uint32_t* d_tile_order = nullptr;
+    uint32_t order_capacity = 0;
+    uint64_t order_sig = 0;
+    bool order_valid = false;
+    uint64_t scene_gen = 0;      // bumped by every rt_scene_upload
     size_t spill_bytes = 0;
     unsigned long long* d_stamps = nullptr;  // RT_FLAG_STAMPS diagnostics
     uint32_t stamp_capacity = 0, stamp_count = 0;
@@ -308,6 +318,9 @@ size_t pool_lds_bytes(uint32_t cap) {
 }
 
 constexpr size_t kLdsPerCu = 160 * 1024;
+// Static LDS of the tracer kernels (s_tile, s_top: 16 B) plus headroom; the
+// code-object metadata (tests/test_isa_budget.py) checks the real value.
+constexpr size_t kStaticLds = 256;
 constexpr size_t kMaxLds = kLdsPerCu - 8 * 1024;  // dynamic LDS of one workgroup (room for static)
 
 struct LaunchShape {
@@ -330,10 +343,8 @@ int blocks_per_cu(rt_context* ctx, bool pool, bool lds_world, size_t lds, int* p
         return RT_OK;
     }
     int api = 0;
-    size_t st = 0;
     RT_HIP(occupancy<R>(pool, lds_world, lds, &api));
-    RT_HIP(static_lds<R>(pool, lds_world, &st));
-    const size_t per_block = (st + lds + 511) / 512 * 512;
+    const size_t per_block = (kStaticLds + lds + 511) / 512 * 512;
     const int by_lds = per_block ? (int)((size_t)kLdsPerCu / per_block) : api;
     *per_cu = std::min(api, by_lds);
     ctx->occ_lds[key] = lds;
@@ -357,10 +368,11 @@ int pool_lds_rays(rt_context* ctx, uint32_t world_lds, uint32_t cap, uint32_t* l
     if (best < 1) best = 1;
     const size_t rec = 7 * sizeof(R) + sizeof(uint32_t);
     const size_t budget = (size_t)kLdsPerCu / (size_t)best;
-    size_t st = 0;
-    RT_HIP(static_lds<R>(true, lw, &st));
-    const size_t fixed = st + world_lds + pool_lds_bytes<R>(0) + 511;
+    const size_t fixed = kStaticLds + world_lds + pool_lds_bytes<R>(0) + 511;
     uint32_t n = budget > fixed ? (uint32_t)((budget - fixed) / rec) : kBlock;
+    // one workgroup's LDS must also stay within the launch limit
+    const size_t room = ctx->lds_per_block > fixed ? ctx->lds_per_block - fixed : 0;
+    n = std::min<uint32_t>(n, (uint32_t)(room / rec));
     n = std::min<uint32_t>(cap, std::max<uint32_t>(kBlock, n & ~31u));
     for (;;) {  // granule rounding: step down until `best` workgroups fit
         int got = 0;
@@ -385,7 +397,7 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
         if (ls.sched == kSchedGrid) {
             // one workgroup per tile: no per-workgroup spill region, so the
             // whole LIFO bound lives in LDS (smaller pop batches if needed)
-            const size_t room = kMaxLds - ls.world_lds;
+            const size_t room = std::min(kMaxLds, ctx->lds_per_block - 4096) - ls.world_lds;
             uint32_t batch = kBlock;
             while (batch > 32 && pool_lds_bytes<R>(pool_capacity(depth, batch)) > room) batch /= 2;
             if (pool_lds_bytes<R>(pool_capacity(depth, batch)) > room)
@@ -406,6 +418,41 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
     ls.grid = ls.sched != kSchedGrid ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, resident)) : n_tiles;
     if (!ls.pool && ls.sched == kSchedStatic && ctx->direct_grid > 0)  // RTC_DIRECT_GRID (A/B)
         ls.grid = std::min<uint32_t>(n_tiles, ctx->direct_grid);
+    return RT_OK;
+}
+
+// Same frame as the last pool launch?  (scene upload, canvas, shard, depth,
+// precision, camera or ray batch)  Then order this launch's tiles by the
+// costs the last one recorded; either way record this launch's costs.
+template <typename R>
+int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* cam, uint32_t depth,
+                    hipStream_t stream) {
+    uint64_t h = 1469598103934665603ull;  // FNV-1a
+    auto mix = [&h](const void* p, size_t n) {
+        const unsigned char* b = static_cast<const unsigned char*>(p);
+        for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    };
+    const uint64_t fields[] = {ctx->scene_gen, P.n_tiles, P.width, P.height, P.shard_index, P.shard_count,
+                               depth, sizeof(R), (uint64_t)(uintptr_t)P.rays, P.n_rays};
+    mix(fields, sizeof(fields));
+    if (cam) mix(cam, sizeof(*cam));
+    if (ctx->order_capacity < P.n_tiles) {
+        (void)hipFree(ctx->d_tile_cost);
+        (void)hipFree(ctx->d_tile_order);
+        ctx->d_tile_cost = ctx->d_tile_order = nullptr;
+        ctx->order_capacity = 0;
+        ctx->order_valid = false;
+        RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_tile_cost), P.n_tiles * sizeof(uint32_t)));
+        RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_tile_order), P.n_tiles * sizeof(uint32_t)));
+        ctx->order_capacity = P.n_tiles;
+    }
+    if (ctx->order_valid && ctx->order_sig == h) {
+        RT_HIP(launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, P.n_tiles, stream));
+        P.tile_order = ctx->d_tile_order;
+    }
+    P.tile_cost = ctx->d_tile_cost;
+    ctx->order_sig = h;
+    ctx->order_valid = true;
     return RT_OK;
 }
 
@@ -466,6 +513,9 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
         P.tile_counter = ctx->d_tile_counter;
         RT_HIP(hipMemsetAsync(ctx->d_tile_counter, 0,
                               (size_t)kTileQueues * kQueueStride * sizeof(unsigned long long), stream));
+        if (ls.pool && ctx->tile_order) {
+            if ((rc = plan_tile_order<R>(ctx, P, cam, depth, stream))) return rc;
+        }
     }
     if (flags & RT_FLAG_STAMPS) {
         if (ctx->stamp_capacity < ls.grid) {
@@ -478,7 +528,11 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
         P.stamps = ctx->d_stamps;
         ctx->stamp_count = ls.grid;
     }
-    RT_HIP(launch_trace<R>(P, ls.pool, ls.grid, ls.lds, stream));
+    if (hipError_t e = launch_trace<R>(P, ls.pool, ls.grid, ls.lds, stream); e != hipSuccess)
+        return set_error(RT_ERR_HIP, std::string("launch of the ") + (ls.pool ? "pool" : "direct") + " kernel (grid " +
+                                         std::to_string(ls.grid) + ", dynamic LDS " + std::to_string(ls.lds) +
+                                         " B, pool " + std::to_string(ls.lcap) + "/" + std::to_string(ls.cap) +
+                                         " rays in LDS): " + hipGetErrorString(e));
     return RT_OK;
 }
 
@@ -575,6 +629,7 @@ int rt_context_create(int device_ordinal, rt_context** out) {
     hipDeviceProp_t prop;
     RT_HIP(hipGetDeviceProperties(&prop, device_ordinal));
     ctx->cu_count = prop.multiProcessorCount;
+    ctx->lds_per_block = prop.sharedMemPerBlock;  // launch limit of static + dynamic LDS
     // scheduling knobs: "grid" (one workgroup per tile, the hardware dispatcher
     // balances), "static" (resident grid, fixed tile stride) or "dynamic"
     // (resident grid + per-XCD atomic tile queues)
@@ -590,6 +645,7 @@ int rt_context_create(int device_ordinal, rt_context** out) {
     if (const char* e = std::getenv("RTC_LDS_WORLD")) ctx->lds_world = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_CULL")) ctx->cull = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_POOL_LDS_RAYS")) ctx->pool_lds_rays = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("RTC_TILE_ORDER")) ctx->tile_order = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_DIRECT_GRID")) ctx->direct_grid = (uint32_t)std::atoi(e);
     RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreate(&ctx->ev_start));
@@ -618,6 +674,8 @@ int rt_context_destroy(rt_context* ctx) {
     (void)hipFree(ctx->d_scratch);
     (void)hipFree(ctx->d_stamps);
     (void)hipFree(ctx->d_spill);
+    (void)hipFree(ctx->d_tile_cost);
+    (void)hipFree(ctx->d_tile_order);
     if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
     if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -643,6 +701,7 @@ int rt_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, c
     }
     ctx->flops.n_lights = nl;
     ctx->have_scene = true;
+    ++ctx->scene_gen;  // invalidates the recorded tile costs
     return RT_OK;
 }
 

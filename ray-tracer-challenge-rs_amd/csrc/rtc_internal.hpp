@@ -158,6 +158,8 @@ struct LaunchParams {
     void* spill;                 // pool overflow: grid x 8 x (pool_capacity - pool_lds_capacity) words
     unsigned long long* stamps;  // RT_FLAG_STAMPS: 2 x grid s_memrealtime values
     unsigned long long* tile_counter;  // kTileQueues queue heads, kQueueStride apart, zeroed per launch
+    const uint32_t* tile_order;        // queue position -> tile (heaviest first), null = raster order
+    uint32_t* tile_cost;               // pool kernel: per-tile duration (10 ns ticks), null = not recorded
     unsigned long long* counters;      // kCounterShards x kNumCounters cumulative u64
     int32_t* error_flag;               // set nonzero on pool overflow
 };

@@ -815,8 +815,8 @@ __device__ inline unsigned int next_tile(const LaunchParams<R>& P, uint32_t it, 
     for (; probe < (uint32_t)kTileQueues; ++probe) {
         const uint32_t q = (blockIdx.x + probe) % kTileQueues;
         const unsigned long long j = atomicAdd(&P.tile_counter[q * kQueueStride], 1ull);
-        const unsigned long long t = q + (unsigned long long)kTileQueues * j;
-        if (t < P.n_tiles) return (unsigned int)t;
+        const unsigned long long i = q + (unsigned long long)kTileQueues * j;
+        if (i < P.n_tiles) return P.tile_order ? P.tile_order[i] : (unsigned int)i;
     }
     return 0xFFFFFFFFu;
 }
@@ -1038,10 +1038,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     Counts k = {};
     const uint32_t tid = threadIdx.x;
     uint32_t probe = 0;
+    unsigned long long tile_start = 0;  // thread 0: s_memrealtime at the tile's start
     for (uint32_t it = 0;; ++it) {
         if (tid == 0) {
             s_tile[it & 1] = next_tile(P, it, probe);
             s_top[0] = 0;
+            tile_start = __builtin_amdgcn_s_memrealtime();
         }
         for (int c = 0; c < 3; ++c) pl.acc[c * kBlock + tid] = 0;
         __syncthreads();
@@ -1103,12 +1105,50 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
                          (R)((double)pl.acc[2 * kBlock + tid] * kAccInvScale)};
         if (valid) store_pixel(P, out_idx, c);
         __syncthreads();  // accumulators are re-zeroed for the next tile
+        // this tile's cost (10 ns ticks) orders the next launch of the same
+        // frame heaviest-first (order_tiles)
+        if (tid == 0 && P.tile_cost)
+            P.tile_cost[t] = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - tile_start, 0xFFFFFFFFull);
     }
     if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
     if (P.stamps) {
         __syncthreads();
         if (threadIdx.x == 0) P.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
     }
+}
+
+// Heaviest-first tile order from the previous launch's per-tile costs: a
+// one-workgroup bucket sort (8 buckets per octave of cost, descending).  The
+// pool kernel's time is set by its last, heaviest tiles (a glass-sphere tile
+// of reflect_refract runs ~400 us); handing those out first bounds the tail
+// (longest-processing-time-first).  Order within a bucket is arbitrary:
+// tiles are independent and pixel sums are fixed-point, so images are not
+// affected.
+constexpr int kOrderBuckets = 256;
+constexpr int kOrderThreads = 1024;
+
+__device__ inline uint32_t cost_bucket(uint32_t c) {  // 0 = heaviest
+    const uint32_t b = (uint32_t)(__builtin_amdgcn_logf((float)c + 1.0f) * 8.0f);
+    return (uint32_t)(kOrderBuckets - 1) - (b < (uint32_t)kOrderBuckets ? b : (uint32_t)(kOrderBuckets - 1));
+}
+
+__global__ __launch_bounds__(kOrderThreads) void order_tiles(const uint32_t* __restrict__ cost,
+                                                             uint32_t* __restrict__ order, uint32_t n) {
+    __shared__ uint32_t hist[kOrderBuckets];
+    for (uint32_t b = threadIdx.x; b < (uint32_t)kOrderBuckets; b += kOrderThreads) hist[b] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) atomicAdd(&hist[cost_bucket(cost[i])], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive scan, 256 entries
+        uint32_t sum = 0;
+        for (int b = 0; b < kOrderBuckets; ++b) {
+            const uint32_t v = hist[b];
+            hist[b] = sum;
+            sum += v;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) order[atomicAdd(&hist[cost_bucket(cost[i])], 1u)] = i;
 }
 
 // De-interleave gathered shard strips into one image.
@@ -1130,6 +1170,9 @@ __global__ void assemble_shards(const unsigned char* __restrict__ gathered, unsi
 // ------------------------------------------------------------ launchers
 template <typename R>
 hipError_t launch_trace(const LaunchParams<R>& P, bool pool, uint32_t grid, size_t dyn_lds, hipStream_t stream) {
+    // hipLaunchKernelGGL reports through hipGetLastError(): drop any stale
+    // error first (every earlier call's own status is checked by the host).
+    (void)hipGetLastError();
     const bool lds = P.world_lds != 0;
 #define RTC_LAUNCH(K, L)                                                                                  \
     hipLaunchKernelGGL((K<R, L>), dim3(grid), dim3(kBlock), dyn_lds, stream, P, P.scene.shapes, P.scene.materials, \
@@ -1154,31 +1197,20 @@ hipError_t occupancy(bool pool, bool lds, size_t dyn_lds, int* blocks_per_cu) {
                : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_direct<R, false>, kBlock, dyn_lds);
 }
 
-// Static LDS of one instantiation (the occupancy API's LDS accounting
-// proved optimistic: it promised 6 pool workgroups/CU where 5 fit).
-template <typename R>
-hipError_t static_lds(bool pool, bool lds, size_t* bytes) {
-    hipFuncAttributes a{};
-    hipError_t e;
-    if (pool)
-        e = lds ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(trace_pool<R, true>))
-                : hipFuncGetAttributes(&a, reinterpret_cast<const void*>(trace_pool<R, false>));
-    else
-        e = lds ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(trace_direct<R, true>))
-                : hipFuncGetAttributes(&a, reinterpret_cast<const void*>(trace_direct<R, false>));
-    *bytes = a.sharedSizeBytes;
-    return e;
-}
-
-template hipError_t static_lds<float>(bool, bool, size_t*);
-template hipError_t static_lds<double>(bool, bool, size_t*);
 template hipError_t launch_trace<float>(const LaunchParams<float>&, bool, uint32_t, size_t, hipStream_t);
 template hipError_t launch_trace<double>(const LaunchParams<double>&, bool, uint32_t, size_t, hipStream_t);
 template hipError_t occupancy<float>(bool, bool, size_t, int*);
 template hipError_t occupancy<double>(bool, bool, size_t, int*);
 
+hipError_t launch_order_tiles(const uint32_t* cost, uint32_t* order, uint32_t n, hipStream_t stream) {
+    (void)hipGetLastError();  // see launch_trace
+    hipLaunchKernelGGL(order_tiles, dim3(1), dim3(kOrderThreads), 0, stream, cost, order, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_assemble(const void* gathered, void* image, uint32_t width, uint32_t height, uint32_t shards,
                            uint32_t strip_rows, uint32_t bpp, hipStream_t stream) {
+    (void)hipGetLastError();  // see launch_trace
     dim3 grid(4, height);
     hipLaunchKernelGGL(assemble_shards, grid, dim3(256), 0, stream, static_cast<const unsigned char*>(gathered),
                        static_cast<unsigned char*>(image), width, height, shards, strip_rows, bpp);

@@ -202,6 +202,22 @@ def test_cull_is_exact(gpu_ctx, rtc, monkeypatch, name, precision):
     assert _counts(sa) == _counts(sb)
 
 
+@pytest.mark.parametrize("name", ["reflect_refract", "cover"])
+def test_cost_ordered_schedule_is_exact(gpu_ctx, rtc, monkeypatch, name):
+    """Repeated launches of one frame run heaviest-tile-first from the last
+    launch's per-tile costs (order_tiles): scheduling only — every ordered
+    render equals the raster-ordered render of a context with RTC_TILE_ORDER=0."""
+    scene = scene_fixture(name)
+    cam = rtc.camera_resize(scene.camera, 256, 160)
+    gpu_ctx.upload(scene)
+    first, s1 = gpu_ctx.render(cam, 6, precision="f32")  # raster order, records costs
+    for _ in range(2):                                   # cost-ordered
+        img, st = gpu_ctx.render(cam, 6, precision="f32")
+        assert np.array_equal(img, first) and _counts(st) == _counts(s1)
+    raster, s0 = _render_with_env(rtc, monkeypatch, {"RTC_TILE_ORDER": "0"}, scene, cam, "f32")
+    assert np.array_equal(raster, first) and _counts(s0) == _counts(s1)
+
+
 @pytest.mark.parametrize("precision", ["f32", "f64"])
 def test_cull_is_exact_for_grazing_rays(gpu_ctx, rtc, monkeypatch, precision):
     """Rays aimed within 1e-6 of sphere and cube silhouettes (rt_color_at

@@ -37,8 +37,9 @@ def kernel_metadata(tmp):
         name = re.search(r"\.name:\s+(\S+)", block)
         vgpr = re.search(r"\.vgpr_count:\s+(\d+)", block)
         priv = re.search(r"\.private_segment_fixed_size:\s+(\d+)", block)
+        group = re.search(r"\.group_segment_fixed_size:\s+(\d+)", block)
         if name and vgpr and priv:
-            kernels[name.group(1)] = (int(vgpr.group(1)), int(priv.group(1)))
+            kernels[name.group(1)] = (int(vgpr.group(1)), int(priv.group(1)), int(group.group(1)) if group else 0)
     return kernels
 
 
@@ -49,6 +50,14 @@ def test_f32_kernels_stay_within_their_occupancy_budget(tmp_path):
     for prefix, (vmax, pmax) in BUDGET.items():
         found = {k: v for k, v in kernels.items() if k.startswith(prefix)}
         assert found, f"no kernel {prefix}* in {LIB}"
-        for name, (vgpr, priv) in found.items():
+        for name, (vgpr, priv, group) in found.items():
             assert vgpr <= vmax, f"{name}: {vgpr} VGPRs > {vmax} (occupancy cliff)"
             assert priv <= pmax, f"{name}: {priv} B/lane of scratch > {pmax}"
+
+
+def test_static_lds_fits_the_hosts_allowance(tmp_path):
+    """rtc_host.cpp sizes LDS residency with kStaticLds = 256 B of static LDS
+    per tracer workgroup; a kernel that declares more would be over-admitted."""
+    for name, (_, _, group) in kernel_metadata(str(tmp_path)).items():
+        if "trace_" in name:
+            assert group <= 256, f"{name}: {group} B of static LDS > kStaticLds"
