@@ -46,7 +46,10 @@ def parse():
     ap.add_argument("--scene", default="three_sphere_scene")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--depth", type=int, default=6, help="World::MAX_REFLECTION_ITERATIONS = 6")
+    ap.add_argument("--depth", type=int, default=None,
+                    help="recursion depth; default 5 for three_sphere_scene (BASELINE configs[1]: 'reflection "
+                         "depth 5' — the scene has no reflective or transparent material, so its rays do not "
+                         "change) and World::MAX_REFLECTION_ITERATIONS = 6 otherwise")
     ap.add_argument("--precision", choices=["f32", "f64"], default="f32")
     ap.add_argument("--mode", choices=["frames", "tiled"], default="frames")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
@@ -95,6 +98,8 @@ def load_traffic(workload: str):
 
 def main():
     args = parse()
+    if args.depth is None:
+        args.depth = 5 if args.scene == "three_sphere_scene" else 6
     import numpy as np
     import torch
     import torch.distributed as dist

@@ -16,7 +16,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SCENES = {"three_sphere": "three_sphere_scene@1920x1080,depth=6,f32",
+SCENES = {"three_sphere": "three_sphere_scene@1920x1080,depth=5,f32",
           "reflect_refract": "reflect_refract@1920x1080,depth=6,f32"}
 
 
