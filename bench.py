@@ -111,8 +111,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BENCH_DIST_BACKEND=gloo and BENCH_SHARE_GPU=1 rehearse the multi-rank
+    # path on a one-GPU box (RCCL refuses two ranks on one device); the
+    # driver's runs use RCCL ("nccl") with one GPU per rank.
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    if os.environ.get("BENCH_SHARE_GPU"):
+        local = local % torch.cuda.device_count()
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
 
     scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{args.scene}.json"))
@@ -180,7 +189,7 @@ def main():
 
     rays = after["rays"] - before["rays"]
     flops = after["algorithmic_flops"] - before["algorithmic_flops"]
-    elapsed, total_rays = rdist.job_totals(elapsed, rays, "cuda")
+    elapsed, total_rays = rdist.job_totals(elapsed, rays, "cuda" if backend == "nccl" else "cpu")
     if rank == 0:
         flops_per_launch = flops / args.steps
         achieved = flops_per_launch / (launch_ms * 1e-3) / 1e12
