@@ -601,8 +601,15 @@ struct Shaded {
     bool patterned = false;  // each light evaluation samples a pattern
     bool refr_eval = false;  // refracted_color past the opaque/depth check
     bool schlick = false;    // schlicks_approximation evaluated
-    V3<R> refl_o, refl_d, refr_o, refr_d;
-    R refl_w, refr_w;  // reflectiveness × {R | 1}, transparency × {1-R | 1}
+};
+
+// Children are handed to push(origin, direction, weight) where they are
+// made (weight: reflectiveness × {R | 1}, transparency × {1-R | 1}), not
+// returned: holding both children until the caller's pushes kept ~14 more
+// values live through the refraction code and forced spills.
+struct NoPush {
+    template <typename V, typename R>
+    __device__ void operator()(V, V, R) const {}
 };
 
 // Count one wave's events after shading (call where every lane arrives):
@@ -620,8 +627,9 @@ __device__ inline void count_events(Counts& k, bool primary, bool hit, const Sha
     k.c[7] += wave_count(hit & sh.schlick);
 }
 
-template <typename R, bool kChildren>
-__device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32_t remaining, Shaded<R>& out) {
+template <typename R, bool kChildren, typename Push = NoPush>
+__device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32_t remaining, Shaded<R>& out,
+                                 Push&& push = Push{}) {
     using T = Real<R>;
     const Hit<R> h = closest_hit(sc, o, d);
     if (h.slot < 0) return false;  // world.rs:85: miss -> BLACK
@@ -695,9 +703,7 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
         }
         if (remaining > 0 && m.reflectiveness != (R)0) {  // world.rs:114-128
             out.refl_child = true;
-            out.refl_o = over;
-            out.refl_d = reflect(d, n);
-            out.refl_w = m.reflectiveness * fr;
+            push(over, reflect(d, n), m.reflectiveness * fr);
         }
         if (remaining > 0 && m.transparency != (R)0) {  // world.rs:130-157
             out.refr_eval = true;
@@ -708,9 +714,8 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
                 const R cos_t = T::sqrt((R)1 - sin2_t);
                 const R f = T::rfma(nr, cos_i, -cos_t);
                 out.refr_child = true;
-                out.refr_o = along(p, n, -T::kOffset);  // under_point, computed_hit.rs:34
-                out.refr_d = {n.x * f - eye.x * nr, n.y * f - eye.y * nr, n.z * f - eye.z * nr};
-                out.refr_w = m.transparency * ft;
+                push(along(p, n, -T::kOffset),  // under_point, computed_hit.rs:34
+                     V3<R>{n.x * f - eye.x * nr, n.y * f - eye.y * nr, n.z * f - eye.z * nr}, m.transparency * ft);
             }
         }
     }
@@ -1074,25 +1079,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
             __syncthreads();  // every lane holds its ray; the next top is set
             Shaded<R> sh;
             bool hit = false;
-            if (active) hit = shade_ray<R, true>(sc, ro, rd, meta >> 8, sh);
-            count_events(k, false, hit, sh, sc.n_lights);
             const uint32_t pix = meta & 0xFFu;
+            const uint32_t child_meta = pix | (((meta >> 8) - 1u) << 8);
+            // lanes spawning a child reserve pool slots together (ballot +
+            // one LDS atomic per wave) at the point the child is made
+            auto push = [&](V3<R> co, V3<R> cd, R cw) {
+                const int slot = wave_reserve(true, &s_top[cur ^ 1]);
+                if (slot < (int)cap) pool_put(pl, slot, co, cd, rw * cw, child_meta);
+                else atomicOr(P.error_flag, 1);
+            };
+            if (active) hit = shade_ray<R, true>(sc, ro, rd, meta >> 8, sh, push);
+            count_events(k, false, hit, sh, sc.n_lights);
             if (hit) {
                 acc_add(pl.acc, pix, (double)(sh.surface.x * rw));
                 acc_add(pl.acc + kBlock, pix, (double)(sh.surface.y * rw));
                 acc_add(pl.acc + 2 * kBlock, pix, (double)(sh.surface.z * rw));
-            }
-            const uint32_t child_meta = pix | (((meta >> 8) - 1u) << 8);
-            const bool c1 = hit && sh.refl_child, c2 = hit && sh.refr_child;
-            const int s1 = wave_reserve(c1, &s_top[cur ^ 1]);
-            const int s2 = wave_reserve(c2, &s_top[cur ^ 1]);
-            if (c1) {
-                if (s1 < (int)cap) pool_put(pl, s1, sh.refl_o, sh.refl_d, rw * sh.refl_w, child_meta);
-                else atomicOr(P.error_flag, 1);
-            }
-            if (c2) {
-                if (s2 < (int)cap) pool_put(pl, s2, sh.refr_o, sh.refr_d, rw * sh.refr_w, child_meta);
-                else atomicOr(P.error_flag, 1);
             }
             __syncthreads();  // pushes complete before the next pop
             if (s_top[cur ^ 1] > (int)cap) {  // overflowed: drop the pool (error already flagged)
