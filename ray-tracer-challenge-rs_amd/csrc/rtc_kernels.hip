@@ -653,12 +653,17 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
         const V3<R> to_light = vsub(lpos, over);
         const R dist = magnitude(to_light);
         const V3<R> ld = normalized(to_light);  // == to_light / dist (world.rs:104-106)
-        const bool shadowed = any_hit(sc, over, ld, dist);
-        // calculate_lighting, material.rs:83-114
+        // calculate_lighting, material.rs:83-114.  The shadow test only
+        // matters where the light is in front of the surface (ldn < 0 gives
+        // ambient only, shadowed or not), so only those lanes trace it; the
+        // reference traces it for every light (world.rs:46-52) and the event
+        // counters still count one shadow ray per light.
+        const R ldn = dot(ld, n);
+        bool shadowed = false;
+        if (!(ldn < (R)0)) shadowed = any_hit(sc, over, ld, dist);
         const V3<R> eff = {base.x * L.intensity[0], base.y * L.intensity[1], base.z * L.intensity[2]};
         V3<R> c = {eff.x * m.ambient, eff.y * m.ambient, eff.z * m.ambient};
         if (!shadowed) {
-            const R ldn = dot(ld, n);
             if (!(ldn < (R)0)) {
                 c = {c.x + (eff.x * m.diffuse) * ldn, c.y + (eff.y * m.diffuse) * ldn,
                      c.z + (eff.z * m.diffuse) * ldn};
