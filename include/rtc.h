@@ -229,6 +229,11 @@ int rt_color_at(rt_context* ctx, const double* rays, uint64_t n_rays,
  * of the last launch made with RT_FLAG_STAMPS; *n = number of workgroups. */
 int rt_debug_stamps(rt_context* ctx, uint64_t* out, uint32_t max_workgroups, uint32_t* n);
 
+/* Diagnostics: per-tile durations (10 ns ticks) the last pool launch
+ * recorded for heaviest-first ordering; *n = entries available (tiles of
+ * the largest pool launch so far, 0 before any). */
+int rt_debug_tile_costs(rt_context* ctx, uint32_t* out, uint32_t max_tiles, uint32_t* n);
+
 /* Cumulative device counters since context creation (after a sync). */
 int rt_read_counters(rt_context* ctx, rt_stats* totals);
 

@@ -817,6 +817,16 @@ int rt_debug_stamps(rt_context* ctx, uint64_t* out, uint32_t max_wg, uint32_t* n
     return RT_OK;
 }
 
+int rt_debug_tile_costs(rt_context* ctx, uint32_t* out, uint32_t max_tiles, uint32_t* n) {
+    if (!ctx || !n) return set_error(RT_ERR_INVALID, "null argument");
+    RT_HIP(hipSetDevice(ctx->device));
+    RT_HIP(hipDeviceSynchronize());
+    *n = ctx->order_valid ? ctx->order_capacity : 0;
+    const uint32_t copy = std::min(max_tiles, *n);
+    if (out && copy) RT_HIP(hipMemcpy(out, ctx->d_tile_cost, copy * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
 int rt_read_counters(rt_context* ctx, rt_stats* totals) {
     if (!ctx || !totals) return set_error(RT_ERR_INVALID, "null argument");
     RT_HIP(hipSetDevice(ctx->device));

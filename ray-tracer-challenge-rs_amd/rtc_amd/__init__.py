@@ -155,6 +155,7 @@ def _load() -> C.CDLL:
                                   P(Stats)]),
         "rt_read_counters": (C.c_int, [C.c_void_p, P(Stats)]),
         "rt_debug_stamps": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_uint32, P(C.c_uint32)]),
+        "rt_debug_tile_costs": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_uint32, P(C.c_uint32)]),
         "rt_assemble_shards": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                          C.c_void_p, C.c_void_p]),
         "rt_scene_load_yaml": (C.c_int, [C.c_char_p, P(C.c_void_p)]),
@@ -179,7 +180,7 @@ _lib = _load()
 EXPORTED_SYMBOLS = (
     "rt_abi_version", "rt_last_error", "rt_device_count", "rt_context_create", "rt_context_destroy",
     "rt_scene_upload", "rt_shard_rows", "rt_render", "rt_render_device", "rt_color_at", "rt_read_counters",
-    "rt_debug_stamps",
+    "rt_debug_stamps", "rt_debug_tile_costs",
     "rt_assemble_shards", "rt_scene_load_yaml", "rt_scene_load_yaml_text", "rt_scene_view_get", "rt_scene_free",
     "rt_camera_make", "rt_camera_resize", "rt_matrix_inverse",
 )
@@ -355,6 +356,14 @@ class Context:
         _check(_lib.rt_debug_stamps(self._h, None, 0, C.byref(n)))
         out = np.zeros((n.value, 2), dtype=np.uint64)
         _check(_lib.rt_debug_stamps(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), n.value, C.byref(n)))
+        return out
+
+    def debug_tile_costs(self) -> np.ndarray:
+        """Per-tile durations (10 ns ticks) recorded by the last pool launch."""
+        n = C.c_uint32(0)
+        _check(_lib.rt_debug_tile_costs(self._h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, dtype=np.uint32)
+        _check(_lib.rt_debug_tile_costs(self._h, out.ctypes.data_as(C.POINTER(C.c_uint32)), n.value, C.byref(n)))
         return out
 
     def counters(self) -> dict:
