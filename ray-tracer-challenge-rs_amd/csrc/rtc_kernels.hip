@@ -841,7 +841,8 @@ template <typename R, bool kLds>
 __device__ inline DevScene<R> scene_view(const LaunchParams<R>& P, const ShapeRec<R>* __restrict__ shapes,
                                          const MaterialRec<R>* __restrict__ materials,
                                          const PatternRec<R>* __restrict__ patterns,
-                                         const LightRec<R>* __restrict__ lights, unsigned char* smem) {
+                                         const LightRec<R>* __restrict__ lights, unsigned char* smem,
+                                         bool stage = false) {
     DevScene<R> sc = P.scene;
     sc.shapes = shapes;
     sc.materials = materials;
@@ -853,16 +854,18 @@ __device__ inline DevScene<R> scene_view(const LaunchParams<R>& P, const ShapeRe
         auto* lm = reinterpret_cast<MaterialRec<R>*>(ls + ns);
         auto* lp = reinterpret_cast<PatternRec<R>*>(lm + sc.n_materials);
         auto* lw = reinterpret_cast<int32_t*>(lp + sc.n_patterns);
-        auto copy = [](void* dst, const void* src, uint32_t bytes) {
-            const uint4* s4 = static_cast<const uint4*>(src);
-            uint4* d4 = static_cast<uint4*>(dst);
-            for (uint32_t i = threadIdx.x; i < bytes / 16; i += kBlock) d4[i] = s4[i];
-        };
-        copy(ls, shapes, ns * (uint32_t)sizeof(ShapeRec<R>));
-        copy(lm, materials, sc.n_materials * (uint32_t)sizeof(MaterialRec<R>));
-        copy(lp, patterns, sc.n_patterns * (uint32_t)sizeof(PatternRec<R>));
-        copy(lw, sc.world_slot, (ns + 3) / 4 * 16);
-        __syncthreads();
+        if (stage) {
+            auto copy = [](void* dst, const void* src, uint32_t bytes) {
+                const uint4* s4 = static_cast<const uint4*>(src);
+                uint4* d4 = static_cast<uint4*>(dst);
+                for (uint32_t i = threadIdx.x; i < bytes / 16; i += kBlock) d4[i] = s4[i];
+            };
+            copy(ls, shapes, ns * (uint32_t)sizeof(ShapeRec<R>));
+            copy(lm, materials, sc.n_materials * (uint32_t)sizeof(MaterialRec<R>));
+            copy(lp, patterns, sc.n_patterns * (uint32_t)sizeof(PatternRec<R>));
+            copy(lw, sc.world_slot, (ns + 3) / 4 * 16);
+            __syncthreads();
+        }
         sc.lworld_slot = lw;
         sc.lshapes = ls;
         sc.lmats = lm;
@@ -874,6 +877,19 @@ __device__ inline DevScene<R> scene_view(const LaunchParams<R>& P, const ShapeRe
         sc.lworld_slot = sc.world_slot;
     }
     return sc;
+}
+
+// The launch's parameters re-read from the kernarg segment (the kernel's
+// first explicit argument starts it).  The asm makes the pointer opaque, so
+// loads through it cannot be hoisted out of the tile loop: scene counts,
+// camera and canvas fields come back as s_loads (scalar cache) where they
+// are used instead of being held in SGPRs for the whole kernel, which spilled
+// ~60 of them into VGPR lanes (v_writelane/v_readlane: VALU issue slots).
+template <typename R>
+__device__ inline const LaunchParams<R>& kernarg_params() {
+    auto k = __builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(k));
+    return *(const LaunchParams<R>*)k;  // address-space cast (constant -> generic)
 }
 
 #define RTC_WORLD_PARAMS(R)                                                                                  \
@@ -902,7 +918,7 @@ template <typename R, bool kLds>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 4 ? RTC_DIRECT_WAVES : 1))) void trace_direct(
     LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
     extern __shared__ __align__(16) unsigned char smem[];
-    const DevScene<R> sc = scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem);
+    (void)scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem, true);
     if (P.stamps && threadIdx.x == 0) P.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     Counts k = {};
     const uint32_t tid = threadIdx.x;
@@ -911,6 +927,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     // grid.  Primary-only tiles cost the same, so no queue is needed, and the
     // tile index is an SGPR by construction (loop control stays scalar).
     for (uint32_t t = blockIdx.x;; t += gridDim.x) {
+        const LaunchParams<R>& P = kernarg_params<R>();
+        const DevScene<R> sc = scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem);
         if (t >= P.n_tiles) break;
         bool valid;
         V3<R> o, d;
@@ -1030,7 +1048,7 @@ template <typename R, bool kLds>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 4 ? RTC_POOL_WAVES : 1))) void trace_pool(
     LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
     extern __shared__ __align__(16) unsigned char smem_all[];
-    const DevScene<R> sc = scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem_all);
+    const DevScene<R> sc = scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem_all, true);
     if (P.stamps && threadIdx.x == 0) P.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     unsigned char* smem = smem_all + (kLds ? P.world_lds : 0);
     __shared__ unsigned int s_tile[2];
