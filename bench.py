@@ -35,6 +35,7 @@ sys.path.insert(0, os.path.join(ROOT, "ray-tracer-challenge-rs_amd"))
 os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
+PEAK_FP64_TFLOPS = 78.6   # FP64 vector: vendor spec (the guide lists FP32 only); the f64 parity path
 PEAK_HBM_GBS = 8000.0
 
 
@@ -192,6 +193,7 @@ def main():
     elapsed, total_rays = rdist.job_totals(elapsed, rays, "cuda" if backend == "nccl" else "cpu")
     if rank == 0:
         flops_per_launch = flops / args.steps
+        peak = PEAK_FP32_TFLOPS if args.precision == "f32" else PEAK_FP64_TFLOPS
         achieved = flops_per_launch / (launch_ms * 1e-3) / 1e12
         workload = f"{args.scene}@{cam.width}x{cam.height},depth={args.depth},{args.precision}"
         traffic = load_traffic(workload)
@@ -211,8 +213,8 @@ def main():
             "config": {"workload": workload, "scene": args.scene, "width": cam.width, "height": cam.height,
                        "max_depth": args.depth, "parallelism": f"{'tiles' if tiled else 'frames'}x{world}",
                        "rays_per_frame": int(rays // args.steps), "mode": args.mode},
-            "roofline": {"bound": "mfma", "pipe": "valu-f32", "achieved": achieved, "peak": PEAK_FP32_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
+            "roofline": {"bound": "mfma", "pipe": f"valu-{args.precision}", "achieved": achieved, "peak": peak,
+                         "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
                          "kernel_ms": launch_ms, "flops_per_launch": flops_per_launch},
         }
         if world == 1 and not args.no_cpu_baseline:
