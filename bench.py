@@ -215,7 +215,11 @@ def main():
                        "rays_per_frame": int(rays // args.steps), "mode": args.mode},
             "roofline": {"bound": "mfma", "pipe": f"valu-{args.precision}", "achieved": achieved, "peak": peak,
                          "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
-                         "kernel_ms": launch_ms, "flops_per_launch": flops_per_launch},
+                         "kernel_ms": launch_ms, "flops_per_launch": flops_per_launch,
+                         # the north star's HBM view: PMC bytes per launch over the launch time,
+                         # against the ~8 TB/s memory roof (a diagnostic: the path is compute-bound)
+                         "hbm_gbs": traffic / (launch_ms * 1e-3) / 1e9 if traffic else None,
+                         "hbm_frac": traffic / (launch_ms * 1e-3) / 1e9 / PEAK_HBM_GBS if traffic else None},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(scene, cam, args.depth, args.cpu_seconds)
