@@ -125,7 +125,12 @@ def main():
             dist.init_process_group(backend)
     torch.cuda.set_device(local)
 
-    scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{args.scene}.json"))
+    # Only rank 0 holds the world, as the reference's single caller does; the
+    # other ranks receive it (an RCCL broadcast).
+    t_first = time.perf_counter()
+    scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{args.scene}.json")) if rank == 0 else None
+    if world > 1:
+        scene = rdist.broadcast_scene(scene, rank, "cuda" if backend == "nccl" else "cpu")
     cam = rtc_amd.camera_resize(scene.camera, args.width, args.height)
     ctx = rtc_amd.Context(local)
     ctx.upload(scene)
@@ -153,6 +158,9 @@ def main():
         if tiled:
             gather()
 
+    step()  # first frame: scene transfer, context, upload and one render
+    torch.cuda.synchronize()
+    first_frame_ms = (time.perf_counter() - t_first) * 1e3
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -221,6 +229,16 @@ def main():
                          "hbm_gbs": traffic / (launch_ms * 1e-3) / 1e9 if traffic else None,
                          "hbm_frac": traffic / (launch_ms * 1e-3) / 1e9 / PEAK_HBM_GBS if traffic else None},
         }
+        line["first_frame_ms"] = first_frame_ms
+        if not tiled:
+            # a drop-in Camera::render: synchronous rt_render into host memory,
+            # PCIe copy included (median of 10; never `value`)
+            lat = []
+            for _ in range(10):
+                t = time.perf_counter()
+                ctx.render(cam, args.depth, args.precision)
+                lat.append((time.perf_counter() - t) * 1e3)
+            line["host_frame_ms"] = float(np.median(lat))
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(scene, cam, args.depth, args.cpu_seconds)
         print(json.dumps(line), flush=True)

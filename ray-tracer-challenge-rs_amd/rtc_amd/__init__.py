@@ -30,6 +30,7 @@ __all__ = [
     "RT_DEFAULT_MAX_DEPTH", "RT_TILE_H", "RT_TILE_W",
 ]
 
+RT_ABI_VERSION = 1  # rtc.h; rt_abi_version() must agree (checked at load)
 RT_TILE_W = 64
 RT_TILE_H = 4
 RT_DEFAULT_MAX_DEPTH = 6  # World::MAX_REFLECTION_ITERATIONS, world.rs:15
@@ -171,6 +172,8 @@ def _load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.rt_abi_version() != RT_ABI_VERSION:
+        raise ImportError(f"rtc_amd: {path} has ABI {lib.rt_abi_version()}, this module expects {RT_ABI_VERSION}")
     return lib
 
 

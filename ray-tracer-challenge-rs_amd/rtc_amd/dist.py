@@ -63,6 +63,60 @@ def gather_strips(strip, gathered, world: int, rank: int, dst: int = 0) -> None:
     dist.gather(strip, chunks, dst=dst)
 
 
+_HEADER = np.dtype([("magic", "<u4"), ("version", "<u4"), ("n", "<u4", 4), ("duplicate_shapes", "<u4")])
+_MAGIC = 0x52544353  # "SCTR"
+
+
+def scene_to_bytes(scene) -> bytes:
+    """The flattened world as one byte string: a header (table counts), then
+    the raw POD tables rt_scene_upload takes and the camera, in that order."""
+    from . import RT_ABI_VERSION
+    hdr = np.zeros((), dtype=_HEADER)
+    hdr["magic"], hdr["version"] = _MAGIC, RT_ABI_VERSION
+    hdr["n"] = scene.counts
+    hdr["duplicate_shapes"] = scene.duplicate_shapes
+    parts = [hdr.tobytes()] + [bytes(t) for t in (scene.shapes, scene.materials, scene.patterns, scene.lights)]
+    return b"".join(parts) + bytes(scene.camera)
+
+
+def scene_from_bytes(data: bytes):
+    """Inverse of scene_to_bytes (bit-exact: the f64 fields are copied raw)."""
+    import ctypes as C
+
+    from . import RT_ABI_VERSION, CameraDesc, LightDesc, MaterialDesc, PatternDesc, SceneTables, ShapeDesc
+    hdr = np.frombuffer(data[:_HEADER.itemsize], dtype=_HEADER)[0]
+    if hdr["magic"] != _MAGIC or hdr["version"] != RT_ABI_VERSION:
+        raise ValueError("not a scene broadcast of this ABI version")
+    off = _HEADER.itemsize
+    tables = []
+    for cls, n in zip((ShapeDesc, MaterialDesc, PatternDesc, LightDesc), hdr["n"]):
+        arr = (cls * int(n))()
+        size = C.sizeof(arr)
+        C.memmove(arr, data[off:off + size], size)
+        tables.append(arr)
+        off += size
+    cam = CameraDesc.from_buffer_copy(data[off:off + C.sizeof(CameraDesc)])
+    if off + C.sizeof(CameraDesc) != len(data):
+        raise ValueError("scene broadcast has the wrong length")
+    return SceneTables(*tables, cam, int(hdr["duplicate_shapes"]))
+
+
+def broadcast_scene(scene, rank: int, device, src: int = 0):
+    """the world only `src` holds (as the reference's
+    single caller does) goes to every rank: its length, then its bytes, as
+    torch.distributed broadcasts (RCCL over xGMI for CUDA `device`, gloo for
+    "cpu").  Every rank returns the same tables; `scene` is ignored off `src`."""
+    import torch
+    import torch.distributed as dist
+    payload = scene_to_bytes(scene) if rank == src else b""
+    n = torch.tensor([len(payload)], dtype=torch.int64, device=device)
+    dist.broadcast(n, src=src)
+    buf = (torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(device) if rank == src
+           else torch.empty(int(n.item()), dtype=torch.uint8, device=device))
+    dist.broadcast(buf, src=src)
+    return scene if rank == src else scene_from_bytes(buf.cpu().numpy().tobytes())
+
+
 def job_totals(elapsed_s: float, rays: float, device) -> tuple[float, float]:
     """(max elapsed over ranks, sum of rays over ranks): the whole-job
     throughput is sum(rays) / max(elapsed)."""

@@ -93,3 +93,44 @@ def test_assemble_host_inverts_the_split():
         st[rows >= 0] = img[rows[rows >= 0]]
         strips.append(st)
     assert np.array_equal(rdist.assemble_host(np.concatenate(strips), h, shards), img)
+
+
+@pytest.mark.parametrize("name", ["three_sphere_scene", "cover", "table", "reflect_refract"])
+def test_scene_bytes_round_trip(name):
+    from rtc_amd import dist as rdist
+    scene = scene_fixture(name)
+    data = rdist.scene_to_bytes(scene)
+    back = rdist.scene_from_bytes(data)
+    assert back.counts == scene.counts and back.duplicate_shapes == scene.duplicate_shapes
+    assert rdist.scene_to_bytes(back) == data  # raw f64 fields: bit-exact
+    with pytest.raises(ValueError):
+        rdist.scene_from_bytes(data[:-1])
+
+
+def _bcast_worker(rank, world, port, name, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from rtc_amd import dist as rdist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        scene = scene_fixture(name) if rank == 0 else None
+        got = rdist.broadcast_scene(scene, rank, "cpu")
+        with open(f"{out_path}.{rank}", "wb") as f:
+            f.write(rdist.scene_to_bytes(got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_broadcast_scene_from_rank0(tmp_path):
+    """only rank 0 holds the world; every rank uploads the same tables."""
+    import torch.multiprocessing as mp
+
+    from rtc_amd import dist as rdist
+    world = 2
+    out = str(tmp_path / "scene")
+    mp.spawn(_bcast_worker, args=(world, _free_port(), "cover", out), nprocs=world, join=True)
+    ref = rdist.scene_to_bytes(scene_fixture("cover"))
+    for r in range(world):
+        assert open(f"{out}.{r}", "rb").read() == ref
