@@ -1,0 +1,47 @@
+"""bench.py's output contract (the driver parses this line every round).
+
+One short run on the GPU at a small canvas: exactly one JSON line with the
+metric, the whole-job value, the roofline object and the CPU baseline, and a
+ray count that matches the reference's semantics for three_sphere (every
+pixel hits a wall or the floor: one primary and one shadow ray per pixel).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config", "roofline"}
+
+
+def _run(*args, timeout=240):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [line for line in r.stdout.splitlines() if line.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_parses_without_a_gpu():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0 and "--gpus" in r.stdout and "--steps" in r.stdout
+
+
+@pytest.mark.gpu
+def test_bench_line_contract():
+    d = _run("--steps", "20", "--warmup", "2", "--width", "320", "--height", "240", "--cpu-seconds", "0.2")
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 1 and d["steps"] == 20 and d["warmup"] == 2 and d["higher_is_better"] is True
+    assert d["unit"] == "Mray/s" and d["dtype"] == "f32" and d["scaling"] == "weak"
+    assert d["config"]["rays_per_frame"] == 2 * 320 * 240
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    rl = d["roofline"]
+    assert rl["unit"] == "TFLOP/s" and rl["peak"] == 157.3 and 0 < rl["frac"] < 1
+    assert abs(rl["frac"] - rl["achieved"] / rl["peak"]) < 1e-12
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
