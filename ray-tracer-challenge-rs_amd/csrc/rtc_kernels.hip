@@ -387,9 +387,11 @@ __device__ inline bool wave_may_hit(const ShapeRec<R>& s, V3<R> o, V3<R> d) {
     // conservative, so no lane that meets the sphere is ever rejected.
     constexpr R kKeep = sizeof(R) == 4 ? (R)(1 - 1e-5) : (R)(1 - 1e-12);
     const R tc = dot(oc, d), oo = dot(oc, oc);
-    const bool front = (tc >= (R)0) | (oo <= r2);
-    const bool lane = front & (Real<R>::madd(oo, kKeep, -r2) * dot(d, d) <= tc * tc);
-    return wave_any(lane);
+    // front = tc >= 0 | oo <= r2, lane = front & line test: one ballot per
+    // comparison, combined as SGPR masks (a ballot of the combined bool makes
+    // the compiler materialise it in a VGPR and compare it again: 2 VALU)
+    const unsigned long long front = __builtin_amdgcn_ballot_w64(tc >= (R)0) | __builtin_amdgcn_ballot_w64(oo <= r2);
+    return (front & __builtin_amdgcn_ballot_w64(Real<R>::madd(oo, kKeep, -r2) * dot(d, d) <= tc * tc)) != 0;
 }
 
 template <typename R>
