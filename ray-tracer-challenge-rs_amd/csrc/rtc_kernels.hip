@@ -25,6 +25,12 @@
 // Two instantiations: R = float (the throughput path) and R = double (parity:
 // the reference's operation order, its FMA sites and EPSILON = 8e-8; the TU
 // is compiled with -ffp-contract=off so nothing else is fused).
+//
+// Kind variants: built a second time with -DRTC_KINDS=<mask of shape kinds>
+// -DRTC_VARIANT=<namespace>, the TU compiles the f32 pool kernel with the
+// shape loops of those kinds only (rtc::<namespace>::launch_trace).  Same
+// code for the kinds it keeps, so the same pixels; the host uses it for
+// worlds whose kinds it covers (rtc_host.cpp, pool_variant).
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -34,6 +40,9 @@
 #include "rtc_internal.hpp"
 
 namespace rtc {
+#ifdef RTC_VARIANT
+namespace RTC_VARIANT {
+#endif
 
 // ------------------------------------------------------------ real traits
 template <typename R>
@@ -351,15 +360,23 @@ __device__ inline void for_kind(const DevScene<R>& sc, F&& f) {
     }
 }
 
+#ifndef RTC_KINDS
+#define RTC_KINDS 63  // every kind
+#endif
+template <typename R, int K, typename F>
+__device__ inline void for_kind_if(const DevScene<R>& sc, F&& f) {
+    if constexpr ((RTC_KINDS >> K) & 1) for_kind<R, K>(sc, f);
+}
+
 template <typename R, typename F>
 __device__ inline void for_all_kinds(const DevScene<R>& sc, F&& f) {
-    for_kind<R, RT_SHAPE_SPHERE>(sc, [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_SPHERE>(s, i); });
-    for_kind<R, RT_SHAPE_PLANE>(sc, [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_PLANE>(s, i); });
-    for_kind<R, RT_SHAPE_CUBE>(sc, [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_CUBE>(s, i); });
-    for_kind<R, RT_SHAPE_CYLINDER>(sc,
+    for_kind_if<R, RT_SHAPE_SPHERE>(sc, [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_SPHERE>(s, i); });
+    for_kind_if<R, RT_SHAPE_PLANE>(sc, [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_PLANE>(s, i); });
+    for_kind_if<R, RT_SHAPE_CUBE>(sc, [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_CUBE>(s, i); });
+    for_kind_if<R, RT_SHAPE_CYLINDER>(sc,
                                    [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_CYLINDER>(s, i); });
-    for_kind<R, RT_SHAPE_CONE>(sc, [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_CONE>(s, i); });
-    for_kind<R, RT_SHAPE_TRIANGLE>(sc,
+    for_kind_if<R, RT_SHAPE_CONE>(sc, [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_CONE>(s, i); });
+    for_kind_if<R, RT_SHAPE_TRIANGLE>(sc,
                                    [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_TRIANGLE>(s, i); });
 }
 
@@ -1207,8 +1224,12 @@ hipError_t launch_trace(const LaunchParams<R>& P, bool pool, uint32_t grid, size
         if (lds) RTC_LAUNCH(trace_pool, true);
         else RTC_LAUNCH(trace_pool, false);
     } else {
+#ifdef RTC_VARIANT
+        return hipErrorInvalidValue;  // kind variants hold the pool kernel only
+#else
         if (lds) RTC_LAUNCH(trace_direct, true);
         else RTC_LAUNCH(trace_direct, false);
+#endif
     }
 #undef RTC_LAUNCH
     return hipGetLastError();
@@ -1219,13 +1240,17 @@ hipError_t occupancy(bool pool, bool lds, size_t dyn_lds, int* blocks_per_cu) {
     if (pool)
         return lds ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_pool<R, true>, kBlock, dyn_lds)
                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_pool<R, false>, kBlock, dyn_lds);
+#ifdef RTC_VARIANT
+    return hipErrorInvalidValue;
+#endif
     return lds ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_direct<R, true>, kBlock, dyn_lds)
                : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_direct<R, false>, kBlock, dyn_lds);
 }
 
 template hipError_t launch_trace<float>(const LaunchParams<float>&, bool, uint32_t, size_t, hipStream_t);
-template hipError_t launch_trace<double>(const LaunchParams<double>&, bool, uint32_t, size_t, hipStream_t);
 template hipError_t occupancy<float>(bool, bool, size_t, int*);
+#ifndef RTC_VARIANT
+template hipError_t launch_trace<double>(const LaunchParams<double>&, bool, uint32_t, size_t, hipStream_t);
 template hipError_t occupancy<double>(bool, bool, size_t, int*);
 
 hipError_t launch_order_tiles(const uint32_t* cost, uint32_t* order, uint32_t n, hipStream_t stream) {
@@ -1243,4 +1268,8 @@ hipError_t launch_assemble(const void* gathered, void* image, uint32_t width, ui
     return hipGetLastError();
 }
 
+#endif  // !RTC_VARIANT
+#ifdef RTC_VARIANT
+}  // namespace RTC_VARIANT
+#endif
 }  // namespace rtc

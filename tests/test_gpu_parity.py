@@ -202,6 +202,19 @@ def test_cull_is_exact(gpu_ctx, rtc, monkeypatch, name, precision):
     assert _counts(sa) == _counts(sb)
 
 
+@pytest.mark.parametrize("name", ["reflect_refract", "refraction"])
+def test_kind_variant_is_exact(gpu_ctx, rtc, monkeypatch, name):
+    """Worlds of spheres and planes run the pool kernel built with only those
+    kinds' loops (rtc_kernels_sp.o): the same frame, bit for bit, as the
+    all-kinds kernel (RTC_KIND_VARIANTS=0), counters included."""
+    scene = scene_fixture(name)
+    cam = rtc.camera_resize(scene.camera, 256, 160)
+    gpu_ctx.upload(scene)
+    a, sa = gpu_ctx.render(cam, 6, precision="f32")
+    b, sb = _render_with_env(rtc, monkeypatch, {"RTC_KIND_VARIANTS": "0"}, scene, cam, "f32")
+    assert np.array_equal(a, b) and _counts(sa) == _counts(sb)
+
+
 @pytest.mark.parametrize("name", ["reflect_refract", "cover"])
 def test_cost_ordered_schedule_is_exact(gpu_ctx, rtc, monkeypatch, name):
     """Repeated launches of one frame run heaviest-tile-first from the last
