@@ -419,6 +419,49 @@ struct Hit {
     int kind;
 };
 
+// Running first minimum of one ray over (t, world order), entries with
+// t >= 0.  f32: (t, world) as one u64 key in a VGPR pair, compared once.
+// tv + 0 maps -0 to +0, so every t >= 0 keys at or below +inf's bits while
+// negative, invalid (-1) and NaN entries key above; the t kept is the
+// entry's own.  The lane-mask form (f64, and f32 under RTC_VALU_KEYS=0)
+// combines four compares bitwise (&& / || would be lowered to divergent
+// branches), and those ANDs/ORs of wave masks are SALU instructions.
+// Same-box A/B, keys vs masks (kernel time): three_sphere -2.8%,
+// shadow_puppets -1.8%, reflect_refract -3.2%, table -1.4%, cover 0.
+#ifndef RTC_VALU_KEYS
+#define RTC_VALU_KEYS 1
+#endif
+template <typename R>
+struct Nearest {
+    static constexpr bool kKeys = sizeof(R) == 4 && RTC_VALU_KEYS;
+    R t = Real<R>::kInf;
+    int w = INT_MAX;
+    unsigned long long key = 0x7F8000007FFFFFFFull;  // (+inf, INT_MAX)
+    __device__ inline void offer(R te, bool v, int we) {
+        if constexpr (kKeys) {
+            const float tv = v ? te : -1.0f;
+            const unsigned long long k = ((unsigned long long)__float_as_uint(tv + 0.0f) << 32) | (uint32_t)we;
+            const bool better = k < key;
+            key = better ? k : key;
+            t = better ? te : t;
+        } else {
+            const bool better = v & (te >= (R)0) & ((te < t) | ((te == t) & (we < w)));
+            t = sel(better, te, t);
+            w = better ? we : w;
+        }
+    }
+    __device__ inline Hit<R> hit(const DevScene<R>& sc) const {
+        const int hw = kKeys ? (int)(uint32_t)key : w;
+        Hit<R> h{t, -1, hw, -1};
+        if (hw != INT_MAX) {
+            const uint32_t ws = (uint32_t)sc.lworld_slot[hw];
+            h.slot = (int)(ws & 0xFFFFFFu);
+            h.kind = (int)(ws >> 24);
+        }
+        return h;
+    }
+};
+
 // collect_intersections + hit (world.rs:25-35, intersections.rs:13-18):
 // the first minimum t >= 0 in (t, world order, push order).  Within one
 // shape a later entry never displaces an equal t (strict `w < world`), so
@@ -426,41 +469,53 @@ struct Hit {
 // slot/kind come from the world_slot table afterwards.
 template <typename R>
 __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
-    R ht = Real<R>::kInf;
-    int hw = INT_MAX;
+    Nearest<R> best;
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
         if (!wave_may_hit(s, o, d)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
         const int w = s.world_index;
-        entries<R, K, true>(s, lo, ld, [&](R t, bool v) {
-            // bitwise, not short-circuit: && / || would be lowered to divergent branches
-            const bool better = v & (t >= (R)0) & ((t < ht) | ((t == ht) & (w < hw)));
-            ht = sel(better, t, ht);
-            hw = better ? w : hw;
-        });
+        entries<R, K, true>(s, lo, ld, [&](R t, bool v) { best.offer(t, v, w); });
     });
-    Hit<R> h{ht, -1, hw, -1};
-    if (hw != INT_MAX) {
-        const uint32_t ws = (uint32_t)sc.lworld_slot[hw];
-        h.slot = (int)(ws & 0xFFFFFFu);
-        h.kind = (int)(ws >> 24);
-    }
-    return h;
+    return best.hit(sc);
 }
+
+// is_in_shadow's test of one ray: some entry with 0 <= t < distance.  f32
+// (RTC_VALU_KEYS): an unsigned min over the bits of (v ? t : -1) + 0 (the +0
+// maps -0 to +0), so entries at t >= 0 order below +inf's bits and negative,
+// invalid and NaN ones above; one compare with the distance at the end
+// replaces three lane-mask AND/ORs per entry.
+template <typename R>
+struct Blocker {
+    static constexpr bool kKeys = sizeof(R) == 4 && RTC_VALU_KEYS;
+    bool hit = false;
+    uint32_t tmin = 0x7F800000u;  // kKeys: bits of the nearest entry at t >= 0
+    __device__ inline void offer(R t, bool v, R dist) {
+        if constexpr (kKeys) {
+            const uint32_t b = __float_as_uint((v ? t : -1.0f) + 0.0f);
+            tmin = b < tmin ? b : tmin;
+        } else {
+            hit |= v & (t >= (R)0) & (t < dist);
+        }
+    }
+    __device__ inline bool blocked(R dist) const {
+        if constexpr (kKeys) return __uint_as_float(tmin) < dist;
+        else return hit;
+    }
+};
 
 // is_in_shadow (world.rs:98-112): any casting shape with 0 <= t < distance.
 template <typename R>
 __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) {
-    bool hit = false;
+    Blocker<R> b;
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
         if (!s.casts_shadow) return;  // wave-uniform
         if (!wave_may_hit(s, o, d)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
-        entries<R, K>(s, lo, ld, [&](R t, bool v) { hit |= v & (t >= (R)0) & (t < dist); });
+        entries<R, K>(s, lo, ld, [&](R t, bool v) { b.offer(t, v, dist); });
     });
-    return hit;
+    return b.blocked(dist);
 }
 
 // Refractive-index containers walk (intersection.rs:33-62) without a list:
@@ -646,25 +701,62 @@ __device__ inline void count_events(Counts& k, bool primary, bool hit, const Sha
     k.c[7] += wave_count(hit & sh.schlick);
 }
 
+// prepare_computations (intersection.rs:21-31) up to the colour the lights
+// see: the hit point, the normal turned toward the eye, over_point
+// (computed_hit.rs:33) and the surface colour there (material.rs:75-80: a
+// pattern is sampled at over_point, once per hit).  Returns the material.
+template <typename R>
+struct Prepared {
+    V3<R> p, n, eye, over, base;
+};
+
+template <typename R>
+__device__ inline const MaterialRec<R>& prepare_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, const Hit<R>& h,
+                                                     Prepared<R>& q, bool& patterned) {
+    const ShapeRec<R>& s = sc.lshapes[h.slot];
+    q.p = along(o, d, h.t);
+    q.n = normal_at(s, h.kind, q.p);
+    q.eye = vneg(d);
+    if (dot(q.n, q.eye) < (R)0) q.n = vneg(q.n);
+    const MaterialRec<R>& m = sc.lmats[s.material];
+    q.over = along(q.p, q.n, Real<R>::kOffset);
+    q.base = {m.color[0], m.color[1], m.color[2]};
+    patterned = m.pattern >= 0;
+    if (patterned) q.base = pattern_color(sc, m.pattern, s, q.over);
+    return m;
+}
+
+// calculate_lighting (material.rs:83-114) of one light: ambient always;
+// diffuse and specular where the light is in front of the surface
+// (ldn = light . normal >= 0) and the point is not shadowed.
+template <typename R>
+__device__ inline V3<R> lighting_term(const LightRec<R>& L, const MaterialRec<R>& m, V3<R> base, V3<R> n, V3<R> eye,
+                                      V3<R> ld, R ldn, bool shadowed) {
+    const V3<R> eff = {base.x * L.intensity[0], base.y * L.intensity[1], base.z * L.intensity[2]};
+    V3<R> c = {eff.x * m.ambient, eff.y * m.ambient, eff.z * m.ambient};
+    if (!shadowed) {
+        if (!(ldn < (R)0)) {
+            c = {c.x + (eff.x * m.diffuse) * ldn, c.y + (eff.y * m.diffuse) * ldn, c.z + (eff.z * m.diffuse) * ldn};
+            const R rde = dot(reflect(vneg(ld), n), eye);
+            if (!(rde <= (R)0)) {
+                const R f = Real<R>::pow(rde, m.shininess);
+                c = {c.x + (L.intensity[0] * m.specular) * f, c.y + (L.intensity[1] * m.specular) * f,
+                     c.z + (L.intensity[2] * m.specular) * f};
+            }
+        }
+    }
+    return c;
+}
+
 template <typename R, bool kChildren, typename Push = NoPush>
 __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32_t remaining, Shaded<R>& out,
                                  Push&& push = Push{}) {
     using T = Real<R>;
     const Hit<R> h = closest_hit(sc, o, d);
     if (h.slot < 0) return false;  // world.rs:85: miss -> BLACK
-    const ShapeRec<R>& s = sc.lshapes[h.slot];
-    // prepare_computations, intersection.rs:21-31
-    const V3<R> p = along(o, d, h.t);
-    V3<R> n = normal_at(s, h.kind, p);
-    const V3<R> eye = vneg(d);
-    if (dot(n, eye) < (R)0) n = vneg(n);
-    const MaterialRec<R>& m = sc.lmats[s.material];
-    const V3<R> over = along(p, n, T::kOffset);  // computed_hit.rs:33
-    // material.rs:75-80: the pattern is sampled at over_point, once per hit
-    V3<R> base = {m.color[0], m.color[1], m.color[2]};
-    const bool patterned = m.pattern >= 0;
-    out.patterned = patterned;
-    if (patterned) base = pattern_color(sc, m.pattern, s, over);
+    Prepared<R> q;
+    const MaterialRec<R>& m = prepare_hit(sc, o, d, h, q, out.patterned);
+    const V3<R> p = q.p, n = q.n, eye = q.eye, over = q.over, base = q.base;
     V3<R> surface = {(R)0, (R)0, (R)0};
     for (int li = 0; li < sc.n_lights; ++li) {
         const LightRec<R> L = ld_uniform(&sc.lights[li]);
@@ -680,20 +772,7 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
         const R ldn = dot(ld, n);
         bool shadowed = false;
         if (!(ldn < (R)0)) shadowed = any_hit(sc, over, ld, dist);
-        const V3<R> eff = {base.x * L.intensity[0], base.y * L.intensity[1], base.z * L.intensity[2]};
-        V3<R> c = {eff.x * m.ambient, eff.y * m.ambient, eff.z * m.ambient};
-        if (!shadowed) {
-            if (!(ldn < (R)0)) {
-                c = {c.x + (eff.x * m.diffuse) * ldn, c.y + (eff.y * m.diffuse) * ldn,
-                     c.z + (eff.z * m.diffuse) * ldn};
-                const R rde = dot(reflect(vneg(ld), n), eye);
-                if (!(rde <= (R)0)) {
-                    const R f = T::pow(rde, m.shininess);
-                    c = {c.x + (L.intensity[0] * m.specular) * f, c.y + (L.intensity[1] * m.specular) * f,
-                         c.z + (L.intensity[2] * m.specular) * f};
-                }
-            }
-        }
+        const V3<R> c = lighting_term(L, m, base, n, eye, ld, ldn, shadowed);
         surface = {surface.x + c.x, surface.y + c.y, surface.z + c.z};
     }
     out.surface = surface;
