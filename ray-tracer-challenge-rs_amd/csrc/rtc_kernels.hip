@@ -998,9 +998,11 @@ __device__ inline const LaunchParams<R>& kernarg_params() {
 // Waves per SIMD the f32 direct kernel is register-limited to (VGPRs <= 512 /
 // waves).  Measured on MI355X, three_sphere 1080p (scripts/ab_builds.sh):
 // 7 (<= 72 VGPRs) 46.0 us, unconstrained (74 VGPRs, 6 waves) 46.5 us,
-// 8 (<= 64 VGPRs, spills at tile level) 48.9 us.
+// 8 (<= 64 VGPRs, spills at tile level) 48.9 us, with SLP vectorization on.
+// Built without it (Makefile) the kernel needs 55 VGPRs, so 8 waves fit
+// without spills: 34.5 us against 34.7 us at 7 waves with SLP.
 #ifndef RTC_DIRECT_WAVES
-#define RTC_DIRECT_WAVES 7
+#define RTC_DIRECT_WAVES 8
 #endif
 // Waves per SIMD of the f32 pool kernel (VGPRs <= 512 / waves; its LDS pool
 // is sized to match, rtc_host.cpp pool_lds_rays).  Occupancy beats spills
