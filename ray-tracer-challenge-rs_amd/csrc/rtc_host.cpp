@@ -35,7 +35,8 @@ hipError_t launch_trace(const LaunchParams<R>& P, bool pool, uint32_t grid, size
 }  // namespace sp
 constexpr uint32_t kKindsSp = (1u << RT_SHAPE_SPHERE) | (1u << RT_SHAPE_PLANE);
 
-hipError_t launch_order_tiles(const uint32_t* cost, uint32_t* order, uint32_t n, hipStream_t stream);
+hipError_t launch_order_tiles(const uint32_t* cost, uint32_t* order, uint32_t n, unsigned long long* heads,
+                              uint32_t n_heads, hipStream_t stream);
 hipError_t launch_assemble(const void* gathered, void* image, uint32_t width, uint32_t height, uint32_t shards,
                            uint32_t strip_rows, uint32_t bpp, hipStream_t stream);
 
@@ -440,9 +441,10 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
 // Same frame as the last pool launch?  (scene upload, canvas, shard, depth,
 // precision, camera or ray batch)  Then order this launch's tiles by the
 // costs the last one recorded; either way record this launch's costs.
+// The ordering kernel also zeroes the queue heads; *heads_zeroed says so.
 template <typename R>
 int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* cam, uint32_t depth,
-                    hipStream_t stream) {
+                    hipStream_t stream, bool* heads_zeroed) {
     uint64_t h = 1469598103934665603ull;  // FNV-1a
     auto mix = [&h](const void* p, size_t n) {
         const unsigned char* b = static_cast<const unsigned char*>(p);
@@ -463,8 +465,10 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
         ctx->order_capacity = P.n_tiles;
     }
     if (ctx->order_valid && ctx->order_sig == h) {
-        RT_HIP(launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, P.n_tiles, stream));
+        RT_HIP(launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, P.n_tiles, ctx->d_tile_counter,
+                                  (uint32_t)(kTileQueues * kQueueStride), stream));
         P.tile_order = ctx->d_tile_order;
+        *heads_zeroed = true;
     }
     P.tile_cost = ctx->d_tile_cost;
     ctx->order_sig = h;
@@ -527,11 +531,13 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     // workgroups' stealing makes a launch's atomic count data-dependent).
     if (ls.sched == kSchedDynamic) {
         P.tile_counter = ctx->d_tile_counter;
-        RT_HIP(hipMemsetAsync(ctx->d_tile_counter, 0,
-                              (size_t)kTileQueues * kQueueStride * sizeof(unsigned long long), stream));
+        bool zeroed = false;
         if (ls.pool && ctx->tile_order) {
-            if ((rc = plan_tile_order<R>(ctx, P, cam, depth, stream))) return rc;
+            if ((rc = plan_tile_order<R>(ctx, P, cam, depth, stream, &zeroed))) return rc;
         }
+        if (!zeroed)
+            RT_HIP(hipMemsetAsync(ctx->d_tile_counter, 0,
+                                  (size_t)kTileQueues * kQueueStride * sizeof(unsigned long long), stream));
     }
     if (flags & RT_FLAG_STAMPS) {
         if (ctx->stamp_capacity < ls.grid) {

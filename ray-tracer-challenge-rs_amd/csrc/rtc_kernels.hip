@@ -1256,21 +1256,35 @@ __device__ inline uint32_t cost_bucket(uint32_t c) {  // 0 = heaviest
     return (uint32_t)(kOrderBuckets - 1) - (b < (uint32_t)kOrderBuckets ? b : (uint32_t)(kOrderBuckets - 1));
 }
 
+// Also zeroes the dynamic schedule's queue heads, so a pool launch with a
+// tile order pays one small launch instead of a memset plus this kernel.
 __global__ __launch_bounds__(kOrderThreads) void order_tiles(const uint32_t* __restrict__ cost,
-                                                             uint32_t* __restrict__ order, uint32_t n) {
+                                                             uint32_t* __restrict__ order, uint32_t n,
+                                                             unsigned long long* __restrict__ heads,
+                                                             uint32_t n_heads) {
     __shared__ uint32_t hist[kOrderBuckets];
+    __shared__ uint32_t scan[kOrderBuckets];
+    for (uint32_t i = threadIdx.x; i < n_heads; i += kOrderThreads) heads[i] = 0ull;
     for (uint32_t b = threadIdx.x; b < (uint32_t)kOrderBuckets; b += kOrderThreads) hist[b] = 0;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) atomicAdd(&hist[cost_bucket(cost[i])], 1u);
     __syncthreads();
-    if (threadIdx.x == 0) {  // exclusive scan, 256 entries
-        uint32_t sum = 0;
-        for (int b = 0; b < kOrderBuckets; ++b) {
-            const uint32_t v = hist[b];
-            hist[b] = sum;
-            sum += v;
-        }
+    // Exclusive scan of the 256 bucket counts: Hillis-Steele over LDS.
+    const uint32_t t = threadIdx.x;
+    uint32_t own = 0;
+    if (t < (uint32_t)kOrderBuckets) {
+        own = hist[t];
+        scan[t] = own;
     }
+    __syncthreads();
+    for (uint32_t off = 1; off < (uint32_t)kOrderBuckets; off <<= 1) {
+        uint32_t v = 0;
+        if (t < (uint32_t)kOrderBuckets && t >= off) v = scan[t - off];
+        __syncthreads();
+        if (t < (uint32_t)kOrderBuckets) scan[t] += v;
+        __syncthreads();
+    }
+    if (t < (uint32_t)kOrderBuckets) hist[t] = scan[t] - own;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) order[atomicAdd(&hist[cost_bucket(cost[i])], 1u)] = i;
 }
@@ -1334,9 +1348,10 @@ template hipError_t occupancy<float>(bool, bool, size_t, int*);
 template hipError_t launch_trace<double>(const LaunchParams<double>&, bool, uint32_t, size_t, hipStream_t);
 template hipError_t occupancy<double>(bool, bool, size_t, int*);
 
-hipError_t launch_order_tiles(const uint32_t* cost, uint32_t* order, uint32_t n, hipStream_t stream) {
+hipError_t launch_order_tiles(const uint32_t* cost, uint32_t* order, uint32_t n, unsigned long long* heads,
+                              uint32_t n_heads, hipStream_t stream) {
     (void)hipGetLastError();  // see launch_trace
-    hipLaunchKernelGGL(order_tiles, dim3(1), dim3(kOrderThreads), 0, stream, cost, order, n);
+    hipLaunchKernelGGL(order_tiles, dim3(1), dim3(kOrderThreads), 0, stream, cost, order, n, heads, n_heads);
     return hipGetLastError();
 }
 
