@@ -2,24 +2,31 @@
 """Benchmark of the MI355X render path — BASELINE.json metric:
 "Mray/s (primary+secondary) and ms/frame at 1920x1080, 1/2/4/8 GPU".
 
-A step is one frame: one launch of the persistent tracer over a 1920x1080
-canvas of the scene (default scenes/three_sphere_scene.yaml = BASELINE
-configs[1]; the YAML's camera with width/height overridden, exactly like
-editing the YAML), scene tables and output buffer resident in HBM.  Rays are
-counted on the device in the reference's semantics (primary +
-shadow + reflect + refract).
+A step is one frame, scene tables and output buffer resident in HBM.  Rays
+are counted on the device in the reference's semantics (SURVEY.md §8d:
+primary + shadow + reflect + refract).
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py ...):
-one process per GPU; frames are independent objects, so each rank renders
-its own frame per step with no data-path collective ("scaling": "weak");
-value = rays of all ranks / max-over-ranks time.  `--mode tiled` instead
-splits ONE frame into cyclic row blocks across ranks and gathers the strips
-to rank 0 over RCCL (the north star's tile split; strong scaling).
+* One GPU (the default): one launch of the persistent tracer over a
+  1920x1080 canvas of scenes/three_sphere_scene.yaml = BASELINE configs[1]
+  (the YAML's camera with width/height overridden, exactly like editing the
+  YAML), f32 framebuffer.
+* N GPUs (python -m torch.distributed.run --nproc-per-node N bench.py
+  --gpus N ...; one process per GPU): by default the north star's image-tile
+  split of BASELINE configs[3] — scenes/cover.yaml at 3840x2160, every frame
+  split across the N GPUs in cyclic row blocks by librtc's own multi-GPU
+  context (csrc/rtc_group.cpp: the scene RCCL-broadcast by rt_scene_upload,
+  the strips RCCL-gathered onto rank 0 and de-interleaved there), gathering
+  the 8-bit canvas (canvas.rs:117-123; 4x fewer bytes than f32).  "scaling":
+  "strong" (one frame per step, whatever N).  The line also carries the same
+  workload on rank 0's GPU alone (`single_gpu_ms_per_step`) and the frame's
+  per-shard render / gather / end-to-end milliseconds.
+  `--mode frames` instead renders an independent frame per rank per step
+  (no data-path collective, "scaling": "weak").
 
 Prints ONE JSON line on rank 0 with the roofline of the tracer kernel (FP32
-compute roof, algorithmic FLOPs of SURVEY.md §8d) and the CPU baseline (the
-f64 oracle = C++ restatement of the reference's rayon render_parallel,
-timed on this host's cores over a bounded sample).
+VALU roof, algorithmic FLOPs of SURVEY.md §8d) and, on one GPU, the CPU
+baseline (the f64 oracle = C++ restatement of the reference's rayon
+render_parallel, timed on this host's cores over a bounded sample).
 """
 from __future__ import annotations
 
@@ -44,15 +51,20 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--scene", default="three_sphere_scene")
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--mode", choices=["auto", "frames", "tiled"], default="auto",
+                    help="auto: one GPU renders frames; N > 1 GPUs split each frame (tiled)")
+    ap.add_argument("--scene", default=None,
+                    help="default three_sphere_scene (configs[1]) on one GPU / in frames mode, cover (configs[3]) "
+                         "when tiled")
+    ap.add_argument("--width", type=int, default=None, help="default 1920 (3840 for the tiled default)")
+    ap.add_argument("--height", type=int, default=None, help="default 1080 (2160 for the tiled default)")
     ap.add_argument("--depth", type=int, default=None,
                     help="recursion depth; default 5 for three_sphere_scene (BASELINE configs[1]: 'reflection "
                          "depth 5' — the scene has no reflective or transparent material, so its rays do not "
                          "change) and World::MAX_REFLECTION_ITERATIONS = 6 otherwise")
     ap.add_argument("--precision", choices=["f32", "f64"], default="f32")
-    ap.add_argument("--mode", choices=["frames", "tiled"], default="frames")
+    ap.add_argument("--out", choices=["real", "u8"], default=None,
+                    help="framebuffer format: default real (f32) on one GPU, u8 (the quantized canvas) when tiled")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--flags", type=int, default=0, help="RT_FLAG_* diagnostic ablations (profiling only)")
@@ -65,6 +77,17 @@ def cpu_threads() -> int:
     except AttributeError:
         n = os.cpu_count() or 1
     return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", n))))
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(scene, cam, depth, budget_s):
@@ -82,7 +105,7 @@ def cpu_baseline(scene, cam, depth, budget_s):
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
-    return {"value": rays / dt / 1e6, "unit": "Mray/s", "cores": threads, "kind": "port",
+    return {"value": rays / dt / 1e6, "unit": "Mray/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
             "sample": f"{frames} full {cam.width}x{cam.height} frame(s) of the same scene, depth {depth}, "
                       f"f64 C++ restatement of Camera::render_parallel, {dt:.1f}s on {threads} threads"}
 
@@ -97,10 +120,20 @@ def load_traffic(workload: str):
         return None
 
 
+def timed_launches(fn, stream, n):
+    """Device milliseconds of n back-to-back calls of fn(), one event pair on `stream`."""
+    import torch
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(n):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1)
+
+
 def main():
     args = parse()
-    if args.depth is None:
-        args.depth = 5 if args.scene == "three_sphere_scene" else 6
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -112,51 +145,52 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # BENCH_DIST_BACKEND=gloo and BENCH_SHARE_GPU=1 rehearse the multi-rank
-    # path on a one-GPU box (RCCL refuses two ranks on one device); the
-    # driver's runs use RCCL ("nccl") with one GPU per rank.
-    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    tiled = args.mode == "tiled" or (args.mode == "auto" and world > 1)
+    if args.scene is None:
+        args.scene = "cover" if tiled else "three_sphere_scene"
+    default_4k = tiled and args.scene == "cover"
+    args.width = args.width or (3840 if default_4k else 1920)
+    args.height = args.height or (2160 if default_4k else 1080)
+    args.out = args.out or ("u8" if tiled else "real")
+    if args.depth is None:
+        args.depth = 5 if args.scene == "three_sphere_scene" else 6
+    # BENCH_SHARE_GPU=1 rehearses several ranks on a one-GPU box (frames mode;
+    # RCCL refuses two ranks on one device, so the tiled group needs one GPU each)
     if os.environ.get("BENCH_SHARE_GPU"):
         local = local % torch.cuda.device_count()
+    # control plane (ids, camera, barriers, max-over-ranks): gloo on the host;
+    # the data path's collectives are librtc's own RCCL calls
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")
     torch.cuda.set_device(local)
 
-    # Only rank 0 holds the world, as the reference's single caller does; the
-    # other ranks receive it (an RCCL broadcast).
+    # Only rank 0 holds the world, as the reference's single caller does
     t_first = time.perf_counter()
     scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{args.scene}.json")) if rank == 0 else None
-    if world > 1:
-        scene = rdist.broadcast_scene(scene, rank, "cuda" if backend == "nccl" else "cpu")
-    cam = rtc_amd.camera_resize(scene.camera, args.width, args.height)
-    ctx = rtc_amd.Context(local)
-    ctx.upload(scene)
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
-    rdtype = torch.float32 if args.precision == "f32" else torch.float64
-    tiled = args.mode == "tiled" and world > 1
+    rdtype = torch.uint8 if args.out == "u8" else (torch.float32 if args.precision == "f32" else torch.float64)
     if tiled:
-        rows = rdist.strip_height(cam.height, world)
-        out = torch.empty((rows, cam.width, 3), dtype=rdtype, device="cuda")
-        gathered = torch.empty((world * rows, cam.width, 3), dtype=rdtype, device="cuda") if rank == 0 else None
+        # the library's multi-GPU context: RCCL communicator from a unique id,
+        # scene broadcast inside rt_scene_upload, strips gathered onto rank 0
+        uid = rdist.share_unique_id(rank) if world > 1 else rtc_amd.comm_unique_id()
+        ctx = rtc_amd.Context.rank(local, world, rank, uid)
+        ctx.upload(scene if rank == 0 else None)
+        cam0 = rtc_amd.camera_resize(scene.camera, args.width, args.height) if rank == 0 else None
+        cam = rdist.share_camera(cam0, rank) if world > 1 else cam0
         image = torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda") if rank == 0 else None
+        out_ptr = image.data_ptr() if rank == 0 else None
     else:
-        out = torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda")
-    shard = (rank, world) if tiled else (0, 1)
-
-    def gather():
-        rdist.gather_strips(out, gathered, world, rank)
-        if rank == 0:
-            ctx.assemble_shards(gathered.data_ptr(), cam.width, cam.height, world, 3 * out.element_size(),
-                                image.data_ptr(), sptr)
+        if world > 1:
+            scene = rdist.broadcast_scene(scene, rank, "cpu")
+        cam = rtc_amd.camera_resize(scene.camera, args.width, args.height)
+        ctx = rtc_amd.Context(local)
+        ctx.upload(scene)
+        image = torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda")
+        out_ptr = image.data_ptr()
 
     def step():
-        ctx.render_device(cam, out.data_ptr(), sptr, args.depth, args.precision, "real", shard, args.flags)
-        if tiled:
-            gather()
+        ctx.render_device(cam, out_ptr, sptr, args.depth, args.precision, args.out, (0, 1), args.flags)
 
     step()  # first frame: scene transfer, context, upload and one render
     torch.cuda.synchronize()
@@ -166,45 +200,63 @@ def main():
     torch.cuda.synchronize()
     before = ctx.counters()
 
-    # Device time of the tracer launches, from HIP events on the launch stream.
-    # Frames mode: ONE event pair brackets the K back-to-back launches (per-launch
-    # event records cost ~6 us of GPU time per frame on MI355X — they stop the
-    # next launch's waves from overlapping the previous one's tail — see
-    # scripts/host_overhead.py), so the average launch duration is the bracket
-    # / K.  Tiled mode: a pair around each render call, excluding the gather.
-    n_ev = args.steps if tiled else 1
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
+    # Device time of the K frames, from one HIP event pair on the launch
+    # stream (per-launch event records cost ~6 us of GPU time per 1080p frame
+    # on MI355X — they stop the next launch's waves from overlapping the
+    # previous one's tail — see scripts/host_overhead.py): average = bracket / K.
+    # Tiled: the bracket is rank 0's stream (its shard, the gather, the de-interleave).
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if tiled:
-        for i in range(args.steps):
-            ev[i][0].record(stream)
-            ctx.render_device(cam, out.data_ptr(), sptr, args.depth, args.precision, "real", shard, args.flags)
-            ev[i][1].record(stream)
-            gather()
-    else:
-        ev[0][0].record(stream)
-        for _ in range(args.steps):
-            step()
-        ev[0][1].record(stream)
-    torch.cuda.synchronize()
+    launch_ms = timed_launches(step, stream, args.steps) / args.steps
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     after = ctx.counters()
-    launch_ms = float(np.sum([a.elapsed_time(b) for a, b in ev])) / args.steps
 
     rays = after["rays"] - before["rays"]
     flops = after["algorithmic_flops"] - before["algorithmic_flops"]
-    elapsed, total_rays = rdist.job_totals(elapsed, rays, "cuda" if backend == "nccl" else "cpu")
+    elapsed, total_rays = rdist.job_totals(elapsed, rays, "cpu")
+    extra = {}
+    if tiled:
+        # per-shard render, gather + de-interleave and end-to-end device ms of
+        # one frame (rt_render's events; median of 5), every rank collective
+        host = np.empty((cam.height, cam.width, 3), dtype=image.cpu().numpy().dtype) if rank == 0 else None
+        sts = [ctx.render_stats(cam, args.depth, args.precision, args.out, host) for _ in range(5)]
+        kernel_ms = float(np.median([st["kernel_ms"] for st in sts]))
+        extra = {"render_ms_per_shard": kernel_ms,
+                 "gather_ms": float(np.median([st["gather_ms"] for st in sts])),
+                 "frame_ms": float(np.median([st["frame_ms"] for st in sts]))}
+        if world > 1:
+            dist.barrier()
+        if rank == 0:
+            # the same workload on rank 0's GPU alone (a single-GPU context)
+            with rtc_amd.Context(local) as one:
+                one.upload(scene)
+                full = torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda")
+                f1 = lambda: one.render_device(cam, full.data_ptr(), sptr, args.depth, args.precision,  # noqa: E731
+                                               args.out)
+                for _ in range(max(2, args.warmup)):
+                    f1()
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                timed_launches(f1, stream, args.steps)
+                single_ms = (time.perf_counter() - t1) * 1e3 / args.steps
+                extra["single_gpu_ms_per_step"] = single_ms
+                extra["speedup_vs_1gpu"] = single_ms / (elapsed * 1e3 / args.steps)
+        if world > 1:
+            dist.barrier()
+    else:
+        kernel_ms = launch_ms
     if rank == 0:
         flops_per_launch = flops / args.steps
         peak = PEAK_FP32_TFLOPS if args.precision == "f32" else PEAK_FP64_TFLOPS
-        achieved = flops_per_launch / (launch_ms * 1e-3) / 1e12
+        achieved = flops_per_launch / (kernel_ms * 1e-3) / 1e12
         workload = f"{args.scene}@{cam.width}x{cam.height},depth={args.depth},{args.precision}"
-        traffic = load_traffic(workload)
+        if args.out == "u8":
+            workload += ",u8"
+        traffic = load_traffic(workload) if not tiled else None
         line = {
             "metric": "Mray/s (primary+secondary) and ms/frame at 1920x1080",
             "value": total_rays / elapsed / 1e6,
@@ -219,24 +271,38 @@ def main():
             "dtype": args.precision,
             "data": "synthetic: the reference's scene (scenes/%s.yaml) rendered at the configured size" % args.scene,
             "config": {"workload": workload, "scene": args.scene, "width": cam.width, "height": cam.height,
-                       "max_depth": args.depth, "parallelism": f"{'tiles' if tiled else 'frames'}x{world}",
-                       "rays_per_frame": int(rays // args.steps), "mode": args.mode},
-            "roofline": {"bound": "mfma", "pipe": f"valu-{args.precision}", "achieved": achieved, "peak": peak,
+                       "max_depth": args.depth, "out": args.out,
+                       "parallelism": f"{'tiles' if tiled else 'frames'}x{world}",
+                       "rays_per_frame": int(total_rays // args.steps) if tiled else int(rays // args.steps),
+                       "mode": "tiled" if tiled else "frames"},
+            # the path is FP32-VALU bound: no MFMA, the compute roof is the vector ALU's
+            "roofline": {"bound": "valu", "pipe": f"valu-{args.precision}", "achieved": achieved, "peak": peak,
                          "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
-                         "kernel_ms": launch_ms, "flops_per_launch": flops_per_launch,
+                         "kernel_ms": kernel_ms, "flops_per_launch": flops_per_launch,
                          # the north star's HBM view: PMC bytes per launch over the launch time,
                          # against the ~8 TB/s memory roof (a diagnostic: the path is compute-bound)
-                         "hbm_gbs": traffic / (launch_ms * 1e-3) / 1e9 if traffic else None,
-                         "hbm_frac": traffic / (launch_ms * 1e-3) / 1e9 / PEAK_HBM_GBS if traffic else None},
+                         "hbm_gbs": traffic / (kernel_ms * 1e-3) / 1e9 if traffic else None,
+                         "hbm_frac": traffic / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS if traffic else None},
         }
+        if tiled:
+            line["roofline"]["kernel"] = "rank 0's shard launch (median of 5 instrumented frames)"
+        line.update(extra)
         line["first_frame_ms"] = first_frame_ms
-        if not tiled:
+        if not tiled and world == 1:
+            if ctx.scene.has_secondary() and args.depth > 0:
+                # cold launch: the first frame after an upload runs tiles in
+                # raster order (no recorded costs to order them heaviest-first)
+                cold = []
+                for _ in range(3):
+                    ctx.upload(scene)
+                    cold.append(timed_launches(step, stream, 1))
+                line["cold_kernel_ms"] = float(np.median(cold))
             # a drop-in Camera::render: synchronous rt_render into host memory,
             # PCIe copy included (median of 10; never `value`)
             lat = []
             for _ in range(10):
                 t = time.perf_counter()
-                ctx.render(cam, args.depth, args.precision)
+                ctx.render(cam, args.depth, args.precision, args.out)
                 lat.append((time.perf_counter() - t) * 1e3)
             line["host_frame_ms"] = float(np.median(lat))
         if world == 1 and not args.no_cpu_baseline:

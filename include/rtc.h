@@ -24,7 +24,12 @@
  *     instead (release profile panic=abort, Cargo.toml:16); a host wrapper
  *     mirroring it turns a negative status into a panic/exception;
  *   - one context drives one GPU and is used from one host thread at a time;
- *     launches of one context are issued on one stream in order;
+ *     its launches are ordered: rt_render / rt_color_at run on the context's
+ *     own stream, rt_render_device on the caller's, and a launch on another
+ *     stream than the previous launch's waits for everything submitted to
+ *     that stream so far.  A stream handed to rt_render_device must stay
+ *     valid until the context's next launch on a different stream (or
+ *     rt_context_destroy);
  *   - there is NO CPU fallback: without a usable HIP device every entry
  *     point that computes returns RT_ERR_NO_DEVICE.
  */
@@ -37,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* Image tile rendered by one workgroup (one wave = one 64-pixel row run, so
  * output stores are contiguous); RT_TILE_H rows are also the row-block unit
@@ -58,7 +63,8 @@ typedef enum rt_status {
     RT_ERR_NO_SCENE = -4,     /* render before rt_scene_upload             */
     RT_ERR_OOM = -5,          /* device allocation failed                  */
     RT_ERR_POOL = -6,         /* device ray pool overflow (never expected) */
-    RT_ERR_IO = -7            /* file / parse error (scene loader)         */
+    RT_ERR_IO = -7,           /* file / parse error (scene loader)         */
+    RT_ERR_COMM = -8          /* RCCL (multi-GPU) call failed              */
 } rt_status;
 
 /* Shape kinds: ray-tracer/src/shapes.rs:1-17 */
@@ -180,8 +186,14 @@ typedef struct rt_stats {
     uint64_t lit_patterned;  /* light evaluations on a patterned material   */
     uint64_t refract_evals;  /* refracted_color past the opaque/depth check */
     uint64_t schlick_evals;  /* schlicks_approximation calls                */
-    double kernel_ms;        /* device time of the render launch            */
+    double kernel_ms;        /* device time of the render launch (multi-GPU: */
+                             /* the slowest shard's)                         */
     double algorithmic_flops;/* SURVEY.md §8d convention                    */
+    double gather_ms;        /* multi-GPU: RCCL gather of the strips + the   */
+                             /* de-interleave on rank 0 (0 on one GPU)       */
+    double frame_ms;         /* device time of the whole frame               */
+    uint32_t n_shards;       /* GPUs the frame was split over                */
+    uint32_t reserved;
 } rt_stats;
 
 typedef struct rt_context rt_context;
@@ -193,6 +205,32 @@ int rt_device_count(int* count);
 int rt_context_create(int device_ordinal, rt_context** out);
 int rt_context_destroy(rt_context* ctx);
 
+/* Multi-GPU contexts (the north star's "image optionally
+ * tiled across 8 GPUs of one node via RCCL broadcast of the scene + gather of
+ * framebuffer strips over xGMI").  A group context splits every frame into
+ * one shard per GPU (cyclic RT_TILE_H-row blocks, rt_shard_rows), gathers the
+ * strips onto rank 0 with RCCL and de-interleaves them there;
+ * rt_scene_upload flattens the world on rank 0 and RCCL-broadcasts the device
+ * tables to every GPU.  The entry points keep their single-GPU meaning:
+ * rt_render / rt_render_device deliver the WHOLE image on rank 0 (so
+ * options.shard_index/shard_count must be 0/1), rt_color_at runs on rank 0.
+ *  - one process driving several GPUs: rt_context_create_multi
+ *    (ncclCommInitAll over `devices`);
+ *  - one process per GPU: rank 0 makes an id with rt_comm_unique_id, the
+ *    caller shares it (any channel), and every rank calls
+ *    rt_context_create_rank (ncclCommInitRank).  Every rank then makes the
+ *    same calls with the same camera and options (collective semantics);
+ *    only rank 0's scene tables and output buffer are used — other ranks may
+ *    pass NULL tables with zero counts and a NULL output.  Counters and stats
+ *    are the calling process's own shards. */
+#define RT_UNIQUE_ID_BYTES 128
+int rt_context_create_multi(const int* devices, int n_devices, rt_context** out);
+int rt_comm_unique_id(uint8_t id[RT_UNIQUE_ID_BYTES]);
+int rt_context_create_rank(int device, int n_ranks, int rank, const uint8_t id[RT_UNIQUE_ID_BYTES],
+                           rt_context** out);
+/* Shards per frame, this context's rank, and the GPUs this process drives. */
+int rt_context_group(rt_context* ctx, int* n_ranks, int* rank, int* local_devices);
+
 /* Flatten + upload a world.  Replaces the World value that Camera::render
  * borrows (camera.rs:79).  Tables are copied; the caller may free them. */
 int rt_scene_upload(rt_context* ctx,
@@ -201,8 +239,13 @@ int rt_scene_upload(rt_context* ctx,
                     const rt_pattern_desc* patterns, uint32_t n_patterns,
                     const rt_light_desc* lights, uint32_t n_lights);
 
-/* Rows of the strip one shard writes (RT_TILE_H-row blocks, cyclic). */
+/* Rows of the strip one shard writes (RT_TILE_H-row blocks, cyclic: tile
+ * row k of the image belongs to shard k % shard_count).  Every strip is
+ * padded to this height (shard 0's), so gathers use equal counts. */
 int rt_shard_rows(uint32_t height, uint32_t shard_count, uint32_t* rows);
+/* For each image row y < height: the shard that renders it and its row in
+ * that shard's strip (the map rt_assemble_shards inverts).  Host only. */
+int rt_shard_row_map(uint32_t height, uint32_t shard_count, uint32_t* shard_of_row, uint32_t* strip_row_of_row);
 
 /* Synchronous render into a caller-owned HOST buffer: Camera::render /
  * render_parallel semantics (camera.rs:79-112).  Output is row-major, y = 0
@@ -233,6 +276,22 @@ int rt_debug_stamps(rt_context* ctx, uint64_t* out, uint32_t max_workgroups, uin
  * recorded for heaviest-first ordering; *n = entries available (tiles of
  * the largest pool launch so far, 0 before any). */
 int rt_debug_tile_costs(rt_context* ctx, uint32_t* out, uint32_t max_tiles, uint32_t* n);
+
+/* Known-answer harness: the device's own per-shape code for the shape at
+ * world index `shape` of the uploaded world, on caller-given inputs (the
+ * reference's per-shape unit tests, e.g. cone.rs:191-252, run on the GPU).
+ * rt_debug_intersect: rays[i] = {ox,oy,oz,dx,dy,dz}; world_space = 0 treats
+ * them as local rays (Intersect::local_intersect), 1 transforms them by the
+ * shape's inverse first (Ray::intersect, ray.rs:45-49).  out[i*5] = entries
+ * the reference pushes (<= RT_DEBUG_MAX_ENTRIES), out[i*5+1..] their t in push
+ * order.  rt_debug_normal: points[i] = {x,y,z}; world_space = 0 gives
+ * local_normal_at (not normalized), 1 gives normal_at (shape.rs:22-27);
+ * out[i*3..] = the normal.  Synchronous; host buffers. */
+#define RT_DEBUG_MAX_ENTRIES 4
+int rt_debug_intersect(rt_context* ctx, uint32_t shape, const double* rays, uint64_t n_rays, uint32_t precision,
+                       uint32_t world_space, double* out);
+int rt_debug_normal(rt_context* ctx, uint32_t shape, const double* points, uint64_t n_points, uint32_t precision,
+                    uint32_t world_space, double* out);
 
 /* Cumulative device counters since context creation (after a sync). */
 int rt_read_counters(rt_context* ctx, rt_stats* totals);

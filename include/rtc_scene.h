@@ -34,9 +34,10 @@ typedef struct rt_scene_view {
     const rt_light_desc* lights;
     uint32_t n_lights;
     rt_camera_desc camera;
-    /* Pairs of value-identical shapes.  The reference identifies shapes by
-     * value in the refraction containers walk (intersection.rs:37-62); the
-     * device identifies them by index.  0 means both agree. */
+    /* Shapes equal by value to an earlier shape (shape.rs:34-38).  The
+     * reference's containers walk identifies shapes by value
+     * (intersection.rs:47); rt_scene_upload gives value-equal shapes one
+     * identity class so the device walk does the same. */
     uint32_t duplicate_shapes;
 } rt_scene_view;
 
@@ -55,6 +56,10 @@ int rt_camera_make(uint32_t width, uint32_t height, double field_of_view,
 /* Re-run Camera::new for a new canvas size, keeping fov and transform —
  * equivalent to editing the YAML camera width/height. */
 int rt_camera_resize(rt_camera_desc* camera, uint32_t width, uint32_t height);
+
+/* Camera::set_transformation (camera.rs:124-127): store the inverse of the
+ * row-major `transform` and update the origin (camera.rs:114-116). */
+int rt_camera_set_transform(rt_camera_desc* camera, const double transform[16]);
 
 /* Matrix<4>::inverse, row-major 16 doubles. */
 int rt_matrix_inverse(const double m[16], double out[16]);

@@ -1,0 +1,152 @@
+// rtc_context.hpp — the per-device state behind an rt_context handle and the
+// host-side internals shared by the single-device entry points
+// (rtc_host.cpp) and the multi-GPU group (rtc_group.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/rtc.h"
+#include "flop_model.hpp"
+#include "rtc_internal.hpp"
+
+namespace rtc {
+
+// World tables cast to R and laid out per kind (rtc_internal.hpp).
+template <typename R>
+struct DeviceWorld {
+    ShapeRec<R>* shapes = nullptr;
+    MaterialRec<R>* materials = nullptr;
+    PatternRec<R>* patterns = nullptr;
+    LightRec<R>* lights = nullptr;
+    int32_t* world_slot = nullptr;
+    DevScene<R> scene{};
+    void release() {
+        (void)hipFree(world_slot);
+        world_slot = nullptr;
+        (void)hipFree(shapes);
+        (void)hipFree(materials);
+        (void)hipFree(patterns);
+        (void)hipFree(lights);
+        shapes = nullptr;
+        materials = nullptr;
+        patterns = nullptr;
+        lights = nullptr;
+    }
+};
+
+}  // namespace rtc
+
+// One device's render state.  A single-device context is one of these; a
+// multi-GPU context (rtc_group.cpp) is the rank-0 member, holding the other
+// devices of the process as `peers`, each member with its own communicator.
+struct rt_context {
+    int device = 0;
+    int cu_count = 0;
+    size_t lds_per_block = 64 * 1024;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    // Stream order across entry points: every launch shares the queue heads,
+    // tile costs/order and pool spill.  rt_render_device runs on the caller's
+    // stream, rt_render/rt_color_at on `stream`; a launch on a stream other
+    // than the previous launch's first makes its stream wait on all work
+    // submitted so far to that one (ev_order recorded at the switch).
+    hipEvent_t ev_order = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool launched = false;
+    unsigned long long* d_tile_counter = nullptr;
+    unsigned long long* d_counters = nullptr;  // kNumCounters cumulative
+    int32_t* d_error = nullptr;
+    bool have_scene = false;
+    rtc::DeviceWorld<float> w32;
+    rtc::DeviceWorld<double> w64;
+    rtc::FlopScene flops;  // per-kind shape counts for the algorithmic FLOP model
+    // Defaults from A/B on MI355X (scripts/ab_sched.sh, scripts/stamps2.sh):
+    // uniform-cost direct tiles -> static stride; high-variance pool tiles ->
+    // per-XCD atomic queues; per-lane stores beat LDS-staged ones (the
+    // staging barriers wait for store completion).
+    uint32_t sched_direct = rtc::kSchedStatic;  // RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic
+    uint32_t sched_pool = rtc::kSchedDynamic;
+    bool lds_world = true;      // RTC_LDS_WORLD=0 gathers shade data from global memory
+    bool cull = true;  // RTC_CULL=0 uploads every shape as unbounded (no wave cull; exactness tests)
+    bool kind_variants = true;  // RTC_KIND_VARIANTS=0: always the all-kinds kernels
+    size_t occ_lds[8] = {};     // occupancy cache: {direct,pool} x {f32,f64} x {global,LDS world}
+    int occ_blocks[8] = {};
+    uint32_t direct_grid = 0;    // RTC_DIRECT_GRID: persistent grid size of the direct kernel (0 = resident)
+    uint32_t pool_lds_rays = 0;  // RTC_POOL_LDS_RAYS: LDS-resident pool slots (0 = sized for occupancy)
+    void* d_spill = nullptr;     // ray-pool overflow regions, one per resident workgroup
+    // Heaviest-first tile order for repeated pool launches of the same frame
+    // (order_tiles): per-tile costs of the last launch and its signature.
+    bool tile_order = true;      // RTC_TILE_ORDER=0: raster order always
+    uint32_t* d_tile_cost = nullptr;
+    uint32_t* d_tile_order = nullptr;
+    uint32_t order_capacity = 0;
+    uint64_t order_sig = 0;
+    bool order_valid = false;
+    uint64_t scene_gen = 0;      // bumped by every rt_scene_upload
+    uint32_t duplicate_shapes = 0;  // shapes value-equal to an earlier one (one identity class)
+    std::vector<int32_t> world_slot;  // world index -> slot | kind << 24 of the uploaded table
+    size_t spill_bytes = 0;
+    unsigned long long* d_stamps = nullptr;  // RT_FLAG_STAMPS diagnostics
+    uint32_t stamp_capacity = 0, stamp_count = 0;
+    void* d_scratch = nullptr;  // host-buffer renders / color_at staging
+    size_t scratch_bytes = 0;
+    // Multi-GPU group (rtc_group.cpp).  A frame is split
+    // into n_ranks shards of cyclic RT_TILE_H-row blocks; this member renders
+    // shard `rank` into d_strip, RCCL gathers the strips onto rank 0, which
+    // de-interleaves them into the image.  Single-device contexts: comm null.
+    ncclComm_t comm = nullptr;
+    int n_ranks = 1, rank = 0;
+    std::vector<rt_context*> peers;  // rank 0 of a one-process group: the other devices' members
+    void* d_strip = nullptr;         // this member's shard strip
+    size_t strip_bytes = 0;
+    void* d_gathered = nullptr;      // rank 0: every strip, shard-major
+    size_t gathered_bytes = 0;
+    hipEvent_t ev_render0 = nullptr, ev_render1 = nullptr, ev_gather1 = nullptr;  // frame timing
+};
+
+namespace rtc {
+
+// rtc_host.cpp
+int create_device_context(int device, rt_context** out);
+void destroy_device_context(rt_context* ctx);
+int check_ready(rt_context* ctx);
+int check_options(const rt_render_options* o);
+int ensure_scratch(rt_context* ctx, size_t bytes);
+int read_counters(rt_context* ctx, unsigned long long out[kNumCounters]);
+void fill_stats(rt_context* ctx, const unsigned long long before[kNumCounters],
+                const unsigned long long after[kNumCounters], float ms, rt_stats* s);
+int check_pool_error(rt_context* ctx);
+uint32_t tile_rows_for(uint32_t height, uint32_t shards, uint32_t shard);
+int validate_scene(const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats, uint32_t nm,
+                   const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights, uint32_t nl);
+// Flatten and upload the world tables to this device (no validation, no sync).
+int build_scene(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats, uint32_t nm,
+                const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights, uint32_t nl);
+// One frame (or shard strip) of this device into `out_device` on `stream`.
+int launch_frame(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, uint32_t shard_index,
+                 uint32_t shard_count, void* out_device, hipStream_t stream);
+// rtc_group.cpp: the same entry points on a multi-GPU context
+int group_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats,
+                       uint32_t nm, const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights,
+                       uint32_t nl);
+int group_render_device(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, void* out_device,
+                        hipStream_t stream);
+int group_render(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, void* out_host,
+                 rt_stats* stats);
+int group_read_counters(rt_context* ctx, rt_stats* totals);
+hipError_t launch_assemble(const void* gathered, void* image, uint32_t width, uint32_t height, uint32_t shards,
+                           uint32_t strip_rows, uint32_t bpp, hipStream_t stream);
+
+#define RT_HIP(call)                                                                               \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return set_error(RT_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));       \
+    } while (0)
+
+}  // namespace rtc

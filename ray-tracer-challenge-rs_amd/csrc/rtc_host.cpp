@@ -20,7 +20,9 @@
 #include "../../include/rtc.h"
 #include "flop_model.hpp"
 #include "host_math.hpp"
+#include "rtc_context.hpp"
 #include "rtc_internal.hpp"
+#include "shape_identity.hpp"
 
 namespace rtc {
 
@@ -37,6 +39,9 @@ constexpr uint32_t kKindsSp = (1u << RT_SHAPE_SPHERE) | (1u << RT_SHAPE_PLANE);
 
 hipError_t launch_order_tiles(const uint32_t* cost, uint32_t* order, uint32_t n, unsigned long long* heads,
                               uint32_t n_heads, hipStream_t stream);
+template <typename R>
+hipError_t launch_debug_shape(const ShapeRec<R>* shapes, int slot, int kind, uint32_t mode, uint32_t world_space,
+                              const double* in, uint32_t n, double* out, hipStream_t stream);
 hipError_t launch_assemble(const void* gathered, void* image, uint32_t width, uint32_t height, uint32_t shards,
                            uint32_t strip_rows, uint32_t bpp, hipStream_t stream);
 
@@ -49,80 +54,8 @@ int set_error(int code, const std::string& msg) {
     return code;
 }
 
-#define RT_HIP(call)                                                                               \
-    do {                                                                                           \
-        hipError_t e_ = (call);                                                                    \
-        if (e_ != hipSuccess)                                                                      \
-            return set_error(RT_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));       \
-    } while (0)
-
-// World tables cast to R and laid out per kind (rtc_internal.hpp).
-template <typename R>
-struct DeviceWorld {
-    ShapeRec<R>* shapes = nullptr;
-    MaterialRec<R>* materials = nullptr;
-    PatternRec<R>* patterns = nullptr;
-    LightRec<R>* lights = nullptr;
-    int32_t* world_slot = nullptr;
-    DevScene<R> scene{};
-    void release() {
-        (void)hipFree(world_slot);
-        world_slot = nullptr;
-        (void)hipFree(shapes);
-        (void)hipFree(materials);
-        (void)hipFree(patterns);
-        (void)hipFree(lights);
-        shapes = nullptr;
-        materials = nullptr;
-        patterns = nullptr;
-        lights = nullptr;
-    }
-};
 
 }  // namespace rtc
-
-struct rt_context {
-    int device = 0;
-    int cu_count = 0;
-    size_t lds_per_block = 64 * 1024;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
-    unsigned long long* d_tile_counter = nullptr;
-    unsigned long long* d_counters = nullptr;  // kNumCounters cumulative
-    int32_t* d_error = nullptr;
-    bool have_scene = false;
-    rtc::DeviceWorld<float> w32;
-    rtc::DeviceWorld<double> w64;
-    rtc::FlopScene flops;  // per-kind shape counts for the algorithmic FLOP model
-    // Defaults from A/B on MI355X (scripts/ab_sched.sh, scripts/stamps2.sh):
-    // uniform-cost direct tiles -> static stride; high-variance pool tiles ->
-    // per-XCD atomic queues; per-lane stores beat LDS-staged ones (the
-    // staging barriers wait for store completion).
-    uint32_t sched_direct = rtc::kSchedStatic;  // RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic
-    uint32_t sched_pool = rtc::kSchedDynamic;
-    bool lds_world = true;      // RTC_LDS_WORLD=0 gathers shade data from global memory
-    bool cull = true;  // RTC_CULL=0 uploads every shape as unbounded (no wave cull; exactness tests)
-    bool kind_variants = true;  // RTC_KIND_VARIANTS=0: always the all-kinds kernels
-    size_t occ_lds[8] = {};     // occupancy cache: {direct,pool} x {f32,f64} x {global,LDS world}
-    int occ_blocks[8] = {};
-    uint32_t direct_grid = 0;    // RTC_DIRECT_GRID: persistent grid size of the direct kernel (0 = resident)
-    uint32_t pool_lds_rays = 0;  // RTC_POOL_LDS_RAYS: LDS-resident pool slots (0 = sized for occupancy)
-    void* d_spill = nullptr;     // ray-pool overflow regions, one per resident workgroup
-    // Heaviest-first tile order for repeated pool launches of the same frame
-    // (order_tiles): per-tile costs of the last launch and its signature.
-    bool tile_order = true;      // RTC_TILE_ORDER=0: raster order always
-    uint32_t* d_tile_cost = nullptr;
-    uint32_t* d_tile_order = nullptr;
-    uint32_t order_capacity = 0;
-    uint64_t order_sig = 0;
-    bool order_valid = false;
-    uint64_t scene_gen = 0;      // bumped by every rt_scene_upload
-    size_t spill_bytes = 0;
-    unsigned long long* d_stamps = nullptr;  // RT_FLAG_STAMPS diagnostics
-    uint32_t stamp_capacity = 0, stamp_count = 0;
-    void* d_scratch = nullptr;  // host-buffer renders / color_at staging
-    size_t scratch_bytes = 0;
-};
 
 namespace rtc {
 namespace {
@@ -137,6 +70,8 @@ int upload(T** dst, const std::vector<T>& v) {
     RT_HIP(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
     return RT_OK;
 }
+
+}  // namespace
 
 // World-space bounding sphere of a shape's intersection set, for the
 // kernels' wave-level cull (wave_may_hit).  Acceleration only: a shape is
@@ -197,18 +132,35 @@ void bounding_sphere(const rt_shape_desc& d, double out[4]) {
     out[3] = wr + pad;
 }
 
+// Device table order: by kind, then by identity class (the world index of
+// the class's first shape), then by world index.  Without value-equal shapes
+// this is world order within each kind.  The tie rule never depends on the
+// table order (the kernels carry world indices), so the order only groups
+// each class's members for the containers walk.
+std::vector<uint32_t> table_order(const rt_shape_desc* shapes, uint32_t ns, const std::vector<uint32_t>& cls) {
+    std::vector<uint32_t> order(ns);
+    for (uint32_t i = 0; i < ns; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        if (shapes[a].kind != shapes[b].kind) return shapes[a].kind < shapes[b].kind;
+        return cls[a] < cls[b];
+    });
+    return order;
+}
+
 template <typename R>
 int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes, uint32_t ns,
                 const rt_material_desc* mats, uint32_t nm, const rt_pattern_desc* pats, uint32_t np,
-                const rt_light_desc* lights, uint32_t nl) {
+                const rt_light_desc* lights, uint32_t nl, const std::vector<uint32_t>& cls) {
     w.release();
     std::vector<ShapeRec<R>> sh;
     std::vector<int32_t> begin(kNumKinds + 1, 0);
+    const std::vector<uint32_t> order = table_order(shapes, ns, cls);
+    size_t next = 0;
     for (int k = 0; k < kNumKinds; ++k) {
         begin[k] = (int32_t)sh.size();
-        for (uint32_t i = 0; i < ns; ++i) {
+        for (; next < order.size() && shapes[order[next]].kind == k; ++next) {
+            const uint32_t i = order[next];
             const rt_shape_desc& d = shapes[i];
-            if (d.kind != k) continue;
             ShapeRec<R> r{};
             for (int q = 0; q < 12; ++q) r.inv[q] = (R)d.inverse[q];
             double bs[4];
@@ -225,7 +177,9 @@ int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes,
             }
             r.world_index = (int32_t)i;
             r.material = d.material;
-            r.closed = d.closed ? 1 : 0;
+            const bool class_end = next + 1 >= order.size() || cls[order[next + 1]] != cls[i];
+            r.flags = (d.closed ? kShapeClosed : 0) | (class_end ? kShapeClassEnd : 0) |
+                      (int32_t)(cls[i] << kShapeClassShift);
             r.casts_shadow = mats[d.material].casts_shadow ? 1 : 0;
             sh.push_back(r);
         }
@@ -275,6 +229,7 @@ int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes,
     if ((rc = upload(&w.shapes, sh)) || (rc = upload(&w.materials, mt)) || (rc = upload(&w.patterns, pt)) ||
         (rc = upload(&w.lights, lt)) || (rc = upload(&w.world_slot, ws)))
         return rc;
+    ctx->world_slot.assign(ws.begin(), ws.begin() + ns);
     w.scene.shapes = w.shapes;
     w.scene.materials = w.materials;
     w.scene.patterns = w.patterns;
@@ -313,8 +268,7 @@ int validate_scene(const rt_shape_desc* shapes, uint32_t ns, const rt_material_d
 }
 
 uint32_t tile_rows_for(uint32_t height, uint32_t shards, uint32_t shard) {
-    const uint32_t trows = (height + RT_TILE_H - 1) / RT_TILE_H;
-    return trows > shard ? (trows - shard + shards - 1) / shards : 0;
+    return shard_tile_rows(height, shards, shard);
 }
 
 // Rays held by the LDS pool for a given depth and pop batch (LIFO bound).
@@ -439,7 +393,7 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
 }
 
 // Same frame as the last pool launch?  (scene upload, canvas, shard, depth,
-// precision, camera or ray batch)  Then order this launch's tiles by the
+// precision, camera; ray batches of rt_color_at are never cost-ordered)  Then order this launch's tiles by the
 // costs the last one recorded; either way record this launch's costs.
 // The ordering kernel also zeroes the queue heads; *heads_zeroed says so.
 template <typename R>
@@ -451,7 +405,7 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
         for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
     };
     const uint64_t fields[] = {ctx->scene_gen, P.n_tiles, P.width, P.height, P.shard_index, P.shard_count,
-                               depth, sizeof(R), (uint64_t)(uintptr_t)P.rays, P.n_rays};
+                               depth, sizeof(R)};
     mix(fields, sizeof(fields));
     if (cam) mix(cam, sizeof(*cam));
     if (ctx->order_capacity < P.n_tiles) {
@@ -507,6 +461,12 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     P.counters = ctx->d_counters;
     P.error_flag = ctx->d_error;
     if (P.n_tiles == 0) return RT_OK;
+    if (ctx->launched && stream != ctx->last_stream) {
+        RT_HIP(hipEventRecord(ctx->ev_order, ctx->last_stream));
+        RT_HIP(hipStreamWaitEvent(stream, ctx->ev_order, 0));
+    }
+    ctx->last_stream = stream;
+    ctx->launched = true;
     LaunchShape ls;
     int rc = plan_launch<R>(ctx, w.scene, depth, P.n_tiles, ls);
     if (rc) return rc;
@@ -532,7 +492,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     if (ls.sched == kSchedDynamic) {
         P.tile_counter = ctx->d_tile_counter;
         bool zeroed = false;
-        if (ls.pool && ctx->tile_order) {
+        if (ls.pool && ctx->tile_order && cam) {  // frames only: a ray batch's content is not in the signature
             if ((rc = plan_tile_order<R>(ctx, P, cam, depth, stream, &zeroed))) return rc;
         }
         if (!zeroed)
@@ -619,6 +579,10 @@ void fill_stats(rt_context* ctx, const unsigned long long before[kNumCounters],
     s->schlick_evals = d[7];
     s->kernel_ms = ms;
     s->algorithmic_flops = algorithmic_flops(ctx->flops, *s);
+    s->gather_ms = 0.0;
+    s->frame_ms = ms;
+    s->n_shards = 1;
+    s->reserved = 0;
 }
 
 int check_pool_error(rt_context* ctx) {
@@ -631,7 +595,6 @@ int check_pool_error(rt_context* ctx) {
     return RT_OK;
 }
 
-}  // namespace
 }  // namespace rtc
 
 using namespace rtc;
@@ -650,7 +613,21 @@ int rt_device_count(int* count) {
     return RT_OK;
 }
 
-int rt_context_create(int device_ordinal, rt_context** out) {
+int rt_context_create(int device_ordinal, rt_context** out) { return create_device_context(device_ordinal, out); }
+
+int rt_context_destroy(rt_context* ctx) {
+    if (!ctx) return RT_OK;
+    for (rt_context* p : ctx->peers) destroy_device_context(p);
+    ctx->peers.clear();
+    destroy_device_context(ctx);
+    return RT_OK;
+}
+
+}  // extern "C"
+
+namespace rtc {
+
+int create_device_context(int device_ordinal, rt_context** out) {
     if (!out) return set_error(RT_ERR_INVALID, "null out");
     *out = nullptr;
     int n = 0;
@@ -685,6 +662,7 @@ int rt_context_create(int device_ordinal, rt_context** out) {
     RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreate(&ctx->ev_start));
     RT_HIP(hipEventCreate(&ctx->ev_stop));
+    RT_HIP(hipEventCreateWithFlags(&ctx->ev_order, hipEventDisableTiming));
     const size_t qbytes = (size_t)kTileQueues * kQueueStride * sizeof(unsigned long long);
     RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_tile_counter), qbytes));
     RT_HIP(hipMemset(ctx->d_tile_counter, 0, qbytes));
@@ -697,10 +675,10 @@ int rt_context_create(int device_ordinal, rt_context** out) {
     return RT_OK;
 }
 
-int rt_context_destroy(rt_context* ctx) {
-    if (!ctx) return RT_OK;
+void destroy_device_context(rt_context* ctx) {
+    if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    (void)hipDeviceSynchronize();  // launches on caller streams too
     ctx->w32.release();
     ctx->w64.release();
     (void)hipFree(ctx->d_tile_counter);
@@ -713,22 +691,44 @@ int rt_context_destroy(rt_context* ctx) {
     (void)hipFree(ctx->d_tile_order);
     if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
     if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
+    if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    (void)hipFree(ctx->d_strip);
+    (void)hipFree(ctx->d_gathered);
+    for (hipEvent_t e : {ctx->ev_render0, ctx->ev_render1, ctx->ev_gather1})
+        if (e) (void)hipEventDestroy(e);
     delete ctx;
-    return RT_OK;
 }
+
+}  // namespace rtc
+
+extern "C" {
 
 int rt_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats,
                     uint32_t nm, const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights,
                     uint32_t nl) {
     if (!ctx) return set_error(RT_ERR_INVALID, "null context");
+    if (ctx->comm) return group_scene_upload(ctx, shapes, ns, mats, nm, pats, np, lights, nl);
     int rc = validate_scene(shapes, ns, mats, nm, pats, np, lights, nl);
     if (rc) return rc;
     RT_HIP(hipSetDevice(ctx->device));
-    RT_HIP(hipStreamSynchronize(ctx->stream));
+    RT_HIP(hipDeviceSynchronize());  // launches on caller streams may still read the old tables
+    return build_scene(ctx, shapes, ns, mats, nm, pats, np, lights, nl);
+}
+
+}  // extern "C"
+
+namespace rtc {
+
+int build_scene(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats, uint32_t nm,
+                const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights, uint32_t nl) {
+    int rc;
     ctx->have_scene = false;
-    if ((rc = build_world<float>(ctx, ctx->w32, shapes, ns, mats, nm, pats, np, lights, nl))) return rc;
-    if ((rc = build_world<double>(ctx, ctx->w64, shapes, ns, mats, nm, pats, np, lights, nl))) return rc;
+    std::vector<uint32_t> cls;  // value-identity classes (shape_identity.hpp)
+    ctx->duplicate_shapes = ident::shape_classes(shapes, ns, mats, pats, cls);
+    if ((rc = build_world<float>(ctx, ctx->w32, shapes, ns, mats, nm, pats, np, lights, nl, cls))) return rc;
+    if ((rc = build_world<double>(ctx, ctx->w64, shapes, ns, mats, nm, pats, np, lights, nl, cls))) return rc;
     ctx->flops = FlopScene{};
     for (uint32_t i = 0; i < ns; ++i) {
         const rt_shape_desc& d = shapes[i];
@@ -740,9 +740,30 @@ int rt_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, c
     return RT_OK;
 }
 
+int launch_frame(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, uint32_t shard_index,
+                 uint32_t shard_count, void* out_device, hipStream_t s) {
+    RT_HIP(hipSetDevice(ctx->device));
+    if (o->precision == RT_PRECISION_F32)
+        return launch<float>(ctx, ctx->w32, cam, nullptr, 0, o->max_depth, o->out_format, shard_index, shard_count,
+                             out_device, s, o->flags);
+    return launch<double>(ctx, ctx->w64, cam, nullptr, 0, o->max_depth, o->out_format, shard_index, shard_count,
+                          out_device, s, o->flags);
+}
+
+}  // namespace rtc
+
+extern "C" {
+
 int rt_shard_rows(uint32_t height, uint32_t shard_count, uint32_t* rows) {
     if (!rows || shard_count == 0) return set_error(RT_ERR_INVALID, "bad arguments");
     *rows = tile_rows_for(height, shard_count, 0) * RT_TILE_H;
+    return RT_OK;
+}
+
+int rt_shard_row_map(uint32_t height, uint32_t shard_count, uint32_t* shard_of_row, uint32_t* strip_row_of_row) {
+    if (shard_count == 0 || (height && (!shard_of_row || !strip_row_of_row)))
+        return set_error(RT_ERR_INVALID, "bad arguments");
+    for (uint32_t y = 0; y < height; ++y) shard_of_image_row(y, shard_count, &shard_of_row[y], &strip_row_of_row[y]);
     return RT_OK;
 }
 
@@ -751,15 +772,12 @@ int rt_render_device(rt_context* ctx, const rt_camera_desc* cam, const rt_render
     int rc = check_ready(ctx);
     if (rc) return rc;
     if ((rc = check_options(o))) return rc;
-    if (!cam || !out_device) return set_error(RT_ERR_INVALID, "null camera or output");
+    if (!cam || (!out_device && !(ctx->comm && ctx->rank != 0)))  // a group's other ranks write no image
+        return set_error(RT_ERR_INVALID, "null camera or output");
     if (cam->width == 0 || cam->height == 0) return RT_OK;  // empty canvas (canvas.rs:27-35)
-    RT_HIP(hipSetDevice(ctx->device));
     hipStream_t s = static_cast<hipStream_t>(hip_stream);  // NULL = HIP's default stream
-    if (o->precision == RT_PRECISION_F32)
-        return launch<float>(ctx, ctx->w32, cam, nullptr, 0, o->max_depth, o->out_format, o->shard_index,
-                             o->shard_count, out_device, s, o->flags);
-    return launch<double>(ctx, ctx->w64, cam, nullptr, 0, o->max_depth, o->out_format, o->shard_index,
-                          o->shard_count, out_device, s, o->flags);
+    if (ctx->comm) return group_render_device(ctx, cam, o, out_device, s);
+    return launch_frame(ctx, cam, o, o->shard_index, o->shard_count, out_device, s);
 }
 
 int rt_render(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, void* out_host,
@@ -767,7 +785,9 @@ int rt_render(rt_context* ctx, const rt_camera_desc* cam, const rt_render_option
     int rc = check_ready(ctx);
     if (rc) return rc;
     if ((rc = check_options(o))) return rc;
-    if (!cam || !out_host) return set_error(RT_ERR_INVALID, "null camera or output");
+    if (!cam) return set_error(RT_ERR_INVALID, "null camera");
+    if (ctx->comm) return group_render(ctx, cam, o, out_host, stats);
+    if (!out_host) return set_error(RT_ERR_INVALID, "null output");
     RT_HIP(hipSetDevice(ctx->device));
     const size_t elem = o->out_format == RT_OUT_U8 ? 1 : (o->precision == RT_PRECISION_F32 ? 4 : 8);
     const uint32_t rows = tile_rows_for(cam->height, o->shard_count, o->shard_index) * RT_TILE_H;
@@ -841,6 +861,51 @@ int rt_color_at(rt_context* ctx, const double* rays, uint64_t n, uint32_t depth,
     return RT_OK;
 }
 
+namespace {
+// rt_debug_intersect / rt_debug_normal: one launch of the KAT harness kernel
+int debug_shape(rt_context* ctx, uint32_t shape, uint32_t mode, const double* in, size_t in_stride, uint64_t n,
+                uint32_t precision, uint32_t world_space, double* out, size_t out_stride) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (!in || !out) return set_error(RT_ERR_INVALID, "null input or output");
+    if (precision > RT_PRECISION_F64) return set_error(RT_ERR_INVALID, "unknown precision");
+    if (shape >= ctx->world_slot.size()) return set_error(RT_ERR_INVALID, "shape index out of range");
+    if (n == 0) return RT_OK;
+    if (n > 0xFFFFFFFFull) return set_error(RT_ERR_INVALID, "too many rays");
+    RT_HIP(hipSetDevice(ctx->device));
+    const size_t in_bytes = n * in_stride * sizeof(double), out_bytes = n * out_stride * sizeof(double);
+    if ((rc = ensure_scratch(ctx, in_bytes + out_bytes))) return rc;
+    double* d_in = static_cast<double*>(ctx->d_scratch);
+    double* d_out = d_in + n * in_stride;
+    RT_HIP(hipMemcpyAsync(d_in, in, in_bytes, hipMemcpyHostToDevice, ctx->stream));
+    const int32_t ws = ctx->world_slot[shape];
+    const int slot = ws & 0xFFFFFF, kind = ws >> 24;
+    if (ctx->launched && ctx->last_stream != ctx->stream) {  // scratch may be in use by nothing else, but keep order
+        RT_HIP(hipEventRecord(ctx->ev_order, ctx->last_stream));
+        RT_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_order, 0));
+    }
+    hipError_t e = precision == RT_PRECISION_F32
+                       ? launch_debug_shape<float>(ctx->w32.shapes, slot, kind, mode, world_space, d_in, (uint32_t)n,
+                                                   d_out, ctx->stream)
+                       : launch_debug_shape<double>(ctx->w64.shapes, slot, kind, mode, world_space, d_in, (uint32_t)n,
+                                                    d_out, ctx->stream);
+    if (e != hipSuccess) return set_error(RT_ERR_HIP, std::string("debug_shape launch: ") + hipGetErrorString(e));
+    RT_HIP(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+}  // namespace
+
+int rt_debug_intersect(rt_context* ctx, uint32_t shape, const double* rays, uint64_t n, uint32_t precision,
+                       uint32_t world_space, double* out) {
+    return debug_shape(ctx, shape, 0, rays, 6, n, precision, world_space, out, 1 + RT_DEBUG_MAX_ENTRIES);
+}
+
+int rt_debug_normal(rt_context* ctx, uint32_t shape, const double* points, uint64_t n, uint32_t precision,
+                    uint32_t world_space, double* out) {
+    return debug_shape(ctx, shape, 1, points, 3, n, precision, world_space, out, 3);
+}
+
 int rt_debug_stamps(rt_context* ctx, uint64_t* out, uint32_t max_wg, uint32_t* n) {
     if (!ctx || !n) return set_error(RT_ERR_INVALID, "null argument");
     RT_HIP(hipSetDevice(ctx->device));
@@ -864,6 +929,7 @@ int rt_debug_tile_costs(rt_context* ctx, uint32_t* out, uint32_t max_tiles, uint
 
 int rt_read_counters(rt_context* ctx, rt_stats* totals) {
     if (!ctx || !totals) return set_error(RT_ERR_INVALID, "null argument");
+    if (!ctx->peers.empty()) return group_read_counters(ctx, totals);
     RT_HIP(hipSetDevice(ctx->device));
     RT_HIP(hipDeviceSynchronize());
     unsigned long long zero[kNumCounters] = {}, now[kNumCounters];

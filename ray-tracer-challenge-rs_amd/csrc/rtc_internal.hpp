@@ -18,9 +18,34 @@
 
 #include "../../include/rtc.h"
 
+#if defined(__HIP__)
+#define RTC_HD __host__ __device__
+#else
+#define RTC_HD
+#endif
+
 namespace rtc {
 
 int set_error(int code, const std::string& msg);  // rtc_host.cpp (thread-local)
+
+// Row-block shards: tile row k of the image (RT_TILE_H rows)
+// belongs to shard k % shards, which renders its tile rows in order into a
+// contiguous strip.  One definition for the kernels' pixel mapping, the
+// de-interleave kernel and the host (rt_shard_row_map, tested on CPU).
+RTC_HD inline uint32_t shard_tile_rows(uint32_t height, uint32_t shards, uint32_t shard) {
+    const uint32_t trows = (height + RT_TILE_H - 1) / RT_TILE_H;
+    return trows > shard ? (trows - shard + shards - 1) / shards : 0;
+}
+// image row of row `strip_row` of shard `shard`'s strip
+RTC_HD inline uint32_t shard_image_row(uint32_t strip_row, uint32_t shards, uint32_t shard) {
+    return ((strip_row / RT_TILE_H) * shards + shard) * RT_TILE_H + strip_row % RT_TILE_H;
+}
+// shard and strip row of image row y (the inverse)
+RTC_HD inline void shard_of_image_row(uint32_t y, uint32_t shards, uint32_t* shard, uint32_t* strip_row) {
+    const uint32_t trow = y / RT_TILE_H;
+    *shard = trow % shards;
+    *strip_row = (trow / shards) * RT_TILE_H + y % RT_TILE_H;
+}
 
 constexpr int kBlock = 256;        // threads per workgroup = 4 waves of 64
 constexpr int kTilePixels = RT_TILE_W * RT_TILE_H;  // one tile per workgroup pass
@@ -55,6 +80,16 @@ constexpr size_t kMaxWorldLds = 16 * 1024;
 constexpr double kAccScale = 281474976710656.0;  // 2^48
 constexpr double kAccInvScale = 1.0 / 281474976710656.0;
 
+// ShapeRec::flags.  Value-equal shapes (shape_identity.hpp) form one identity
+// class; its members are adjacent within their kind's run of the table, the
+// last one carries kShapeClassEnd, and every member carries the class id (the
+// world index of its first member), so the containers walk can toggle one
+// entry per class as the reference does (intersection.rs:47).  A world with
+// no value-equal shapes has one class per shape, each its own world index.
+constexpr int32_t kShapeClosed = 1;    // cylinder/cone `closed`
+constexpr int32_t kShapeClassEnd = 2;  // last member of its identity class
+constexpr int kShapeClassShift = 8;
+
 template <typename R>
 struct alignas(16) ShapeRec {
     R inv[12];     // rows 0..2 of transformation_inverse (row 3 is never read:
@@ -66,7 +101,7 @@ struct alignas(16) ShapeRec {
     int32_t world_index;
     int32_t casts_shadow;  // material.casts_shadow, hoisted for the any-hit loop
     int32_t material;
-    int32_t closed;
+    int32_t flags;  // kShapeClosed | kShapeClassEnd | identity class << kShapeClassShift
     R ymin, ymax;  // cylinder/cone min/max (cylinder.rs:12-14)
     R tri[12];     // triangle vertex_1, edge_1, edge_2, normal (triangle.rs:12-17)
 };

@@ -317,7 +317,7 @@ __device__ inline void entries(const ShapeRec<R>& s, V3<R> o, V3<R> d, F&& emit)
             quadratic<R>(a, b, c, !single, side);
         }
         // intersect_caps: cylinder.rs:41-58 / cone.rs:41-58
-        const bool caps = s.closed && !(T::fabs(d.y) < T::kEps);
+        const bool caps = (s.flags & kShapeClosed) && !(T::fabs(d.y) < T::kEps);
         const R r_lo = (K == RT_SHAPE_CYLINDER) ? (R)1 : ymin * ymin;
         const R r_hi = (K == RT_SHAPE_CYLINDER) ? (R)1 : ymax * ymax;
         R t = T::div(ymin - o.y, d.y);
@@ -518,10 +518,17 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) 
     return b.blocked(dist);
 }
 
-// Refractive-index containers walk (intersection.rs:33-62) without a list:
-// a shape is inside the container list iff an odd number of its entries sort
-// before the hit; the list's `last()` is the present shape whose last entry
-// before the hit sorts latest.  Keys sort by (t, world order, push order).
+// Refractive-index containers walk (intersection.rs:33-62) without a list.
+// The list holds at most one member of each identity class (value-equal
+// shapes, rtc_internal.hpp kShapeClassEnd): an entry of a shape removes the
+// class's member if one is present (position() compares by value,
+// intersection.rs:47) and pushes the shape otherwise.  So a class is in the
+// list at the hit iff an odd number of its members' entries sort before the
+// hit, and the list's `last()` is the present class whose latest such entry
+// sorts latest.  Keys sort by (t, world order, push order).  Members of a
+// class are adjacent in the table, so the count and latest key run over a
+// class's records and are settled at its last one; with no value-equal
+// shapes every record ends its own class.
 template <typename R>
 __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> d, const Hit<R>& h, R& n1,
                                           R& n2) {
@@ -535,15 +542,17 @@ __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> 
     // The hit's own entry is the first of its shape at t == h.t, so entries
     // of that shape sort before it iff t < h.t: push order 0 says exactly that.
     const Key hk{h.t, h.world, 0};
+    const uint32_t hit_class = (uint32_t)sc.lshapes[h.slot].flags >> kShapeClassShift;
     bool have_all = false, have_other = false, hit_present = false;
     Key best_all{}, best_other{};
     int mat_all = -1, mat_other = -1;
+    int count = 0;  // entries before the hit of the current class
+    Key last{};     // the latest of them
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
         const int w = s.world_index;
-        int e = 0, count = 0;
-        Key last{};
+        int e = 0;
         entries<R, K>(s, lo, ld, [&](R t, bool v) {
             const Key k{t, w, e};
             if (v && before(k, hk)) {
@@ -552,13 +561,14 @@ __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> 
             }
             e += v ? 1 : 0;
         });
+        if (!(s.flags & kShapeClassEnd)) return;  // wave-uniform: more members follow
         if (count & 1) {
             if (!have_all || before(best_all, last)) {
                 best_all = last;
                 mat_all = s.material;
                 have_all = true;
             }
-            if (slot == h.slot) {
+            if ((uint32_t)s.flags >> kShapeClassShift == hit_class) {
                 hit_present = true;
             } else if (!have_other || before(best_other, last)) {
                 best_other = last;
@@ -566,19 +576,19 @@ __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> 
                 have_other = true;
             }
         }
+        count = 0;
     });
     n1 = have_all ? sc.lmats[mat_all].refractive_index : (R)1;
-    if (hit_present)  // the hit removes itself from the list
+    if (hit_present)  // the hit's class leaves the list
         n2 = have_other ? sc.lmats[mat_other].refractive_index : (R)1;
     else              // the hit pushes itself
         n2 = sc.lmats[sc.lshapes[h.slot].material].refractive_index;
 }
 
-// shape.rs:22-27 + local_normal_at of each shape
+// local_normal_at of each shape (object space, not normalized)
 template <typename R>
-__device__ inline V3<R> normal_at(const ShapeRec<R>& s, int kind, V3<R> p) {
+__device__ inline V3<R> local_normal(const ShapeRec<R>& s, int kind, V3<R> lp) {
     using T = Real<R>;
-    const V3<R> lp = xform_point(s.inv, p);
     V3<R> ln;
     switch (kind) {
         case RT_SHAPE_SPHERE: ln = lp; break;                          // sphere.rs:57-59
@@ -612,7 +622,13 @@ __device__ inline V3<R> normal_at(const ShapeRec<R>& s, int kind, V3<R> p) {
         }
         default: ln = {s.tri[9], s.tri[10], s.tri[11]}; break;  // triangle.rs:78-80
     }
-    return normalized(xform_normal(s.inv, ln));
+    return ln;
+}
+
+// shape.rs:22-27: world point -> object point -> local normal -> world normal
+template <typename R>
+__device__ inline V3<R> normal_at(const ShapeRec<R>& s, int kind, V3<R> p) {
+    return normalized(xform_normal(s.inv, local_normal(s, kind, xform_point(s.inv, p))));
 }
 
 // Pattern::color_at_shape (pattern.rs:10-14) and the five color_at bodies.
@@ -869,10 +885,9 @@ template <typename R>
 __device__ inline bool tile_pixel(const LaunchParams<R>& P, uint32_t t, uint32_t tid, uint32_t& x, uint32_t& y,
                                   uint64_t& out_idx) {
     const uint32_t lrow = t / P.tiles_x, tcol = t - lrow * P.tiles_x;
-    const uint32_t grow = lrow * P.shard_count + P.shard_index;
+    const uint32_t local_y = lrow * RT_TILE_H + (tid / RT_TILE_W);  // row in this shard's strip
     x = tcol * RT_TILE_W + (tid % RT_TILE_W);
-    y = grow * RT_TILE_H + (tid / RT_TILE_W);
-    const uint32_t local_y = lrow * RT_TILE_H + (tid / RT_TILE_W);
+    y = shard_image_row(local_y, P.shard_count, P.shard_index);
     out_idx = (uint64_t)local_y * P.width + x;
     return x < P.width && y < P.height;
 }
@@ -912,7 +927,9 @@ __device__ inline void flush_counts(const Counts& k, unsigned long long* global)
 // others in turn: without stealing, a queue whose tiles were cheap left its
 // XCD idle while another XCD's queue ran 300-450 us longer (reflect_refract,
 // per-workgroup timestamps).  The heads are zeroed before every launch that
-// uses them (a stream-ordered memset), so their atomics need no bookkeeping.
+// uses them, stream-ordered: by order_tiles on a cost-ordered pool launch,
+// by a memset otherwise (rtc_host.cpp launch), so their atomics need no
+// bookkeeping.
 template <typename R>
 __device__ inline unsigned int next_tile(const LaunchParams<R>& P, uint32_t it, uint32_t& probe) {
     if (P.persistent == kSchedGrid) return it == 0 ? blockIdx.x : 0xFFFFFFFFu;
@@ -1296,13 +1313,62 @@ __global__ void assemble_shards(const unsigned char* __restrict__ gathered, unsi
     const uint64_t row_bytes = (uint64_t)width * bpp;
     const uint32_t y = blockIdx.y;
     if (y >= height) return;
-    const uint32_t trow = y / RT_TILE_H, within = y % RT_TILE_H;
-    const uint32_t shard = trow % shards, local_trow = trow / shards;
-    const uint64_t src_row = (uint64_t)shard * strip_rows + (uint64_t)local_trow * RT_TILE_H + within;
+    uint32_t shard, strip_row;
+    shard_of_image_row(y, shards, &shard, &strip_row);
+    const uint64_t src_row = (uint64_t)shard * strip_rows + strip_row;
     const unsigned char* src = gathered + src_row * row_bytes;
     unsigned char* dst = image + (uint64_t)y * row_bytes;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < row_bytes; i += (uint64_t)gridDim.x * blockDim.x)
         dst[i] = src[i];
+}
+
+// Known-answer harness (rt_debug_intersect / rt_debug_normal): the product's
+// own per-shape device code on caller-given rays or points, so the
+// reference's per-shape unit tests (sphere.rs, plane.rs, cube.rs, cylinder.rs,
+// cone.rs, triangle.rs, ray.rs) run against the GPU.  mode 0: intersect
+// (every entry the reference pushes, in push order; world_space transforms
+// the ray by the shape's inverse first, ray.rs:45-49, else the ray is
+// already local as in local_intersect); mode 1: normal (world_space:
+// normal_at, shape.rs:22-27; else local_normal_at).
+constexpr int kDebugMaxEntries = RT_DEBUG_MAX_ENTRIES;
+
+template <typename R>
+__global__ void debug_shape(const ShapeRec<R>* __restrict__ shapes, int slot, int kind, uint32_t mode,
+                            uint32_t world_space, const double* __restrict__ in, uint32_t n,
+                            double* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const ShapeRec<R> s = shapes[slot];
+    if (mode == 0) {
+        const double* q = in + 6 * (size_t)i;
+        V3<R> o = {(R)q[0], (R)q[1], (R)q[2]}, d = {(R)q[3], (R)q[4], (R)q[5]};
+        if (world_space) {
+            const V3<R> lo = xform_point(s.inv, o), ld = xform_vector(s.inv, d);
+            o = lo;
+            d = ld;
+        }
+        double* r = out + (1 + kDebugMaxEntries) * (size_t)i;
+        int c = 0;
+        auto emit = [&](R t, bool v) {
+            if (v && c < kDebugMaxEntries) r[1 + c++] = (double)t;
+        };
+        switch (kind) {
+            case RT_SHAPE_SPHERE: entries<R, RT_SHAPE_SPHERE>(s, o, d, emit); break;
+            case RT_SHAPE_PLANE: entries<R, RT_SHAPE_PLANE>(s, o, d, emit); break;
+            case RT_SHAPE_CUBE: entries<R, RT_SHAPE_CUBE>(s, o, d, emit); break;
+            case RT_SHAPE_CYLINDER: entries<R, RT_SHAPE_CYLINDER>(s, o, d, emit); break;
+            case RT_SHAPE_CONE: entries<R, RT_SHAPE_CONE>(s, o, d, emit); break;
+            default: entries<R, RT_SHAPE_TRIANGLE>(s, o, d, emit); break;
+        }
+        r[0] = (double)c;
+    } else {
+        const double* q = in + 3 * (size_t)i;
+        const V3<R> p = {(R)q[0], (R)q[1], (R)q[2]};
+        const V3<R> nv = world_space ? normal_at(s, kind, p) : local_normal(s, kind, p);
+        out[3 * (size_t)i] = (double)nv.x;
+        out[3 * (size_t)i + 1] = (double)nv.y;
+        out[3 * (size_t)i + 2] = (double)nv.z;
+    }
 }
 
 // ------------------------------------------------------------ launchers
@@ -1354,6 +1420,19 @@ hipError_t launch_order_tiles(const uint32_t* cost, uint32_t* order, uint32_t n,
     hipLaunchKernelGGL(order_tiles, dim3(1), dim3(kOrderThreads), 0, stream, cost, order, n, heads, n_heads);
     return hipGetLastError();
 }
+
+template <typename R>
+hipError_t launch_debug_shape(const ShapeRec<R>* shapes, int slot, int kind, uint32_t mode, uint32_t world_space,
+                              const double* in, uint32_t n, double* out, hipStream_t stream) {
+    (void)hipGetLastError();  // see launch_trace
+    hipLaunchKernelGGL(debug_shape<R>, dim3((n + 255) / 256), dim3(256), 0, stream, shapes, slot, kind, mode,
+                       world_space, in, n, out);
+    return hipGetLastError();
+}
+template hipError_t launch_debug_shape<float>(const ShapeRec<float>*, int, int, uint32_t, uint32_t, const double*,
+                                              uint32_t, double*, hipStream_t);
+template hipError_t launch_debug_shape<double>(const ShapeRec<double>*, int, int, uint32_t, uint32_t, const double*,
+                                               uint32_t, double*, hipStream_t);
 
 hipError_t launch_assemble(const void* gathered, void* image, uint32_t width, uint32_t height, uint32_t shards,
                            uint32_t strip_rows, uint32_t bpp, hipStream_t stream) {

@@ -30,6 +30,7 @@
 #include "../../include/rtc_scene.h"
 #include "host_math.hpp"
 #include "rtc_internal.hpp"
+#include "shape_identity.hpp"
 
 namespace rtc {
 namespace {
@@ -688,32 +689,6 @@ struct SceneTables {
     uint32_t duplicates = 0;
 };
 
-static bool pattern_value_eq(const std::vector<rt_pattern_desc>& P, int a, int b) {
-    if (a == b) return true;
-    if (a < 0 || b < 0) return false;
-    const rt_pattern_desc &x = P[a], &y = P[b];
-    return x.kind == y.kind && std::memcmp(x.color_a, y.color_a, sizeof(x.color_a)) == 0 &&
-           std::memcmp(x.color_b, y.color_b, sizeof(x.color_b)) == 0 &&
-           std::memcmp(x.inverse, y.inverse, sizeof(x.inverse)) == 0;
-}
-
-// Value equality of two loaded shapes (shape.rs:34-38, derive(PartialEq)).
-static bool shape_value_eq(const SceneTables& t, const rt_shape_desc& a, const rt_shape_desc& b) {
-    if (a.kind != b.kind) return false;
-    for (int k = 0; k < 16; ++k)
-        if (!(a.inverse[k] == b.inverse[k])) return false;
-    if ((a.kind == RT_SHAPE_CONE || a.kind == RT_SHAPE_CYLINDER) &&
-        !(a.minimum == b.minimum && a.maximum == b.maximum && a.closed == b.closed))
-        return false;
-    const rt_material_desc &m = t.materials[a.material], &n = t.materials[b.material];
-    for (int k = 0; k < 3; ++k)
-        if (!(m.color[k] == n.color[k])) return false;
-    return m.ambient == n.ambient && m.diffuse == n.diffuse && m.specular == n.specular &&
-           m.shininess == n.shininess && m.reflectiveness == n.reflectiveness && m.transparency == n.transparency &&
-           m.refractive_index == n.refractive_index && m.casts_shadow == n.casts_shadow &&
-           pattern_value_eq(t.patterns, m.pattern, n.pattern);
-}
-
 static void load_text(const std::string& text, SceneTables& out) {
     Parser p(text);
     Node doc = p.parse_document();
@@ -745,9 +720,11 @@ static void load_text(const std::string& text, SceneTables& out) {
         }
         out.shapes[k].material = idx;
     }
-    for (size_t a = 0; a < out.shapes.size(); ++a)
-        for (size_t b = a + 1; b < out.shapes.size(); ++b)
-            if (shape_value_eq(out, out.shapes[a], out.shapes[b])) out.duplicates++;
+    // shapes equal by value to an earlier one (shape.rs:34-38); rt_scene_upload
+    // gives such shapes one identity class, as the containers walk does
+    std::vector<uint32_t> cls;
+    out.duplicates = ident::shape_classes(out.shapes.data(), (uint32_t)out.shapes.size(), out.materials.data(),
+                                          out.patterns.data(), cls);
 }
 
 }  // namespace rtc
@@ -823,6 +800,19 @@ int rt_camera_resize(rt_camera_desc* cam, uint32_t width, uint32_t height) {
     cam->half_width = s.half_width;
     cam->half_height = s.half_height;
     cam->pixel_size = s.pixel_size;
+    return RT_OK;
+}
+
+int rt_camera_set_transform(rt_camera_desc* cam, const double t[16]) {
+    if (!cam || !t) return rtc::set_error(RT_ERR_INVALID, "rt_camera_set_transform: null argument");
+    rtc::hm::M4 a;
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) a.m[r][c] = t[4 * r + c];
+    const rtc::hm::M4 inv = rtc::hm::inverse(a);  // camera.rs:124-127
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) cam->inverse[4 * r + c] = inv.m[r][c];
+    const double o[3] = {0, 0, 0};
+    rtc::hm::mul_point(inv, o, cam->origin);  // update_origin, camera.rs:114-116
     return RT_OK;
 }
 

@@ -26,11 +26,11 @@ import numpy as np
 
 __all__ = [
     "RenderError", "lib_path", "abi_version", "device_count", "matrix_inverse", "camera_make",
-    "camera_resize", "load_scene", "load_scene_text", "SceneTables", "Context", "shard_rows",
+    "camera_resize", "camera_set_transform", "load_scene", "load_scene_text", "SceneTables", "Context", "shard_rows",
     "RT_DEFAULT_MAX_DEPTH", "RT_TILE_H", "RT_TILE_W",
 ]
 
-RT_ABI_VERSION = 1  # rtc.h; rt_abi_version() must agree (checked at load)
+RT_ABI_VERSION = 2  # rtc.h; rt_abi_version() must agree (checked at load)
 RT_TILE_W = 64
 RT_TILE_H = 4
 RT_DEFAULT_MAX_DEPTH = 6  # World::MAX_REFLECTION_ITERATIONS, world.rs:15
@@ -38,11 +38,14 @@ RT_MAX_SUPPORTED_DEPTH = 16
 
 RT_OK = 0
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_HIP", -3: "RT_ERR_NO_DEVICE", -4: "RT_ERR_NO_SCENE",
-          -5: "RT_ERR_OOM", -6: "RT_ERR_POOL", -7: "RT_ERR_IO"}
+          -5: "RT_ERR_OOM", -6: "RT_ERR_POOL", -7: "RT_ERR_IO", -8: "RT_ERR_COMM"}
+RT_UNIQUE_ID_BYTES = 128
 
 SHAPE_KINDS = {"sphere": 0, "plane": 1, "cube": 2, "cylinder": 3, "cone": 4, "triangle": 5}
 PATTERN_KINDS = {"stripe": 0, "gradient": 1, "ring": 2, "checker": 3, "complex": 4, "test": 5}
 PRECISIONS = {"f32": 0, "f64": 1}
+# rt_render_options.flags: diagnostic ablations (rtc.h); never in a parity or bench result
+RT_FLAG_NO_COUNTERS, RT_FLAG_NO_SHADE, RT_FLAG_NO_TRACE, RT_FLAG_STAMPS = 1, 2, 4, 8
 OUT_FORMATS = {"real": 0, "u8": 1}
 
 
@@ -96,7 +99,8 @@ class Stats(C.Structure):
     _fields_ = [("primary", C.c_uint64), ("shadow", C.c_uint64), ("reflect", C.c_uint64),
                 ("refract", C.c_uint64), ("shaded", C.c_uint64), ("lit_patterned", C.c_uint64),
                 ("refract_evals", C.c_uint64), ("schlick_evals", C.c_uint64), ("kernel_ms", C.c_double),
-                ("algorithmic_flops", C.c_double)]
+                ("algorithmic_flops", C.c_double), ("gather_ms", C.c_double), ("frame_ms", C.c_double),
+                ("n_shards", C.c_uint32), ("reserved", C.c_uint32)]
 
     def as_dict(self) -> dict:
         d = {name: getattr(self, name) for name, _ in self._fields_}
@@ -167,6 +171,16 @@ def _load() -> C.CDLL:
                                      P(C.c_double), P(CameraDesc)]),
         "rt_camera_resize": (C.c_int, [P(CameraDesc), C.c_uint32, C.c_uint32]),
         "rt_matrix_inverse": (C.c_int, [P(C.c_double), P(C.c_double)]),
+        "rt_camera_set_transform": (C.c_int, [P(CameraDesc), P(C.c_double)]),
+        "rt_shard_row_map": (C.c_int, [C.c_uint32, C.c_uint32, P(C.c_uint32), P(C.c_uint32)]),
+        "rt_context_create_multi": (C.c_int, [P(C.c_int), C.c_int, P(C.c_void_p)]),
+        "rt_comm_unique_id": (C.c_int, [P(C.c_uint8)]),
+        "rt_context_create_rank": (C.c_int, [C.c_int, C.c_int, C.c_int, P(C.c_uint8), P(C.c_void_p)]),
+        "rt_context_group": (C.c_int, [C.c_void_p, P(C.c_int), P(C.c_int), P(C.c_int)]),
+        "rt_debug_intersect": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), C.c_uint64, C.c_uint32, C.c_uint32,
+                                         P(C.c_double)]),
+        "rt_debug_normal": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), C.c_uint64, C.c_uint32, C.c_uint32,
+                                      P(C.c_double)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -183,7 +197,8 @@ _lib = _load()
 EXPORTED_SYMBOLS = (
     "rt_abi_version", "rt_last_error", "rt_device_count", "rt_context_create", "rt_context_destroy",
     "rt_scene_upload", "rt_shard_rows", "rt_render", "rt_render_device", "rt_color_at", "rt_read_counters",
-    "rt_debug_stamps", "rt_debug_tile_costs",
+    "rt_debug_stamps", "rt_debug_tile_costs", "rt_debug_intersect", "rt_debug_normal", "rt_camera_set_transform",
+    "rt_shard_row_map", "rt_context_create_multi", "rt_comm_unique_id", "rt_context_create_rank", "rt_context_group",
     "rt_assemble_shards", "rt_scene_load_yaml", "rt_scene_load_yaml_text", "rt_scene_view_get", "rt_scene_free",
     "rt_camera_make", "rt_camera_resize", "rt_matrix_inverse",
 )
@@ -220,6 +235,14 @@ def camera_make(width: int, height: int, fov: float, frm, to, up) -> CameraDesc:
     return cam
 
 
+def camera_set_transform(cam: CameraDesc, transform) -> CameraDesc:
+    """Camera::set_transformation (camera.rs:124-127) on a copy: inverse + origin."""
+    c = cam.copy()
+    t = (C.c_double * 16)(*np.asarray(transform, dtype=np.float64).reshape(16))
+    _check(_lib.rt_camera_set_transform(C.byref(c), t))
+    return c
+
+
 def camera_resize(cam: CameraDesc, width: int, height: int) -> CameraDesc:
     """Camera::new for another canvas size, same fov/transform (= editing YAML width/height)."""
     c = cam.copy()
@@ -231,6 +254,22 @@ def shard_rows(height: int, shard_count: int) -> int:
     r = C.c_uint32(0)
     _check(_lib.rt_shard_rows(height, shard_count, C.byref(r)))
     return r.value
+
+
+def shard_row_map(height: int, shard_count: int):
+    """(shard, strip row) of every image row (rtc.h rt_shard_row_map; host only)."""
+    shard = np.zeros(height, dtype=np.uint32)
+    row = np.zeros(height, dtype=np.uint32)
+    _check(_lib.rt_shard_row_map(height, shard_count, shard.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                 row.ctypes.data_as(C.POINTER(C.c_uint32))))
+    return shard, row
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id for rt_context_create_rank (rank 0 makes it, the caller shares it)."""
+    buf = (C.c_uint8 * RT_UNIQUE_ID_BYTES)()
+    _check(_lib.rt_comm_unique_id(buf))
+    return bytes(buf)
 
 
 @dataclass
@@ -290,12 +329,38 @@ def load_scene_text(text: str) -> SceneTables:
 class Context:
     """One GPU.  Mirrors the borrow in Camera::render(&self, world: &World)."""
 
-    def __init__(self, device: int = 0):
-        h = C.c_void_p()
-        _check(_lib.rt_context_create(device, C.byref(h)))
+    def __init__(self, device: int = 0, _handle: C.c_void_p | None = None):
+        h = _handle
+        if h is None:
+            h = C.c_void_p()
+            _check(_lib.rt_context_create(device, C.byref(h)))
         self._h = h
         self.device = device
         self.scene: SceneTables | None = None
+
+    @classmethod
+    def multi(cls, devices) -> "Context":
+        """One process, several GPUs (rt_context_create_multi: ncclCommInitAll).  Frames are split in
+        row-block shards across the devices and gathered onto devices[0]."""
+        arr = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        _check(_lib.rt_context_create_multi(arr, len(devices), C.byref(h)))
+        return cls(devices[0], h)
+
+    @classmethod
+    def rank(cls, device: int, n_ranks: int, rank: int, unique_id: bytes) -> "Context":
+        """One process per GPU (rt_context_create_rank: ncclCommInitRank); every rank then makes the same
+        calls; rank 0's scene and output are the ones used."""
+        buf = (C.c_uint8 * RT_UNIQUE_ID_BYTES).from_buffer_copy(unique_id)
+        h = C.c_void_p()
+        _check(_lib.rt_context_create_rank(device, n_ranks, rank, buf, C.byref(h)))
+        return cls(device, h)
+
+    def group(self):
+        """(shards per frame, this context's rank, GPUs driven by this process)."""
+        n, r, loc = C.c_int(), C.c_int(), C.c_int()
+        _check(_lib.rt_context_group(self._h, C.byref(n), C.byref(r), C.byref(loc)))
+        return n.value, r.value, loc.value
 
     def close(self) -> None:
         if self._h:
@@ -314,8 +379,12 @@ class Context:
         except Exception:
             pass
 
-    def upload(self, scene: SceneTables) -> None:
-        _check(_lib.rt_scene_upload(self._h, *scene.args()))
+    def upload(self, scene: SceneTables | None) -> None:
+        """rt_scene_upload; on a non-zero rank of a group, None (the scene comes from rank 0)."""
+        if scene is None:
+            _check(_lib.rt_scene_upload(self._h, None, 0, None, 0, None, 0, None, 0))
+        else:
+            _check(_lib.rt_scene_upload(self._h, *scene.args()))
         self.scene = scene
 
     @staticmethod
@@ -335,13 +404,22 @@ class Context:
                               C.byref(st)))
         return img, st.as_dict()
 
+    def render_stats(self, camera: CameraDesc, depth: int = RT_DEFAULT_MAX_DEPTH, precision: str = "f32",
+                     out_format: str = "real", out=None):
+        """rt_render into `out` (a host array of the frame, or None on a group's non-zero ranks): stats only."""
+        opts = self.options(depth, precision, out_format)
+        st = Stats()
+        ptr = None if out is None else out.ctypes.data_as(C.c_void_p)
+        _check(_lib.rt_render(self._h, C.byref(camera), C.byref(opts), ptr, C.byref(st)))
+        return st.as_dict()
+
     def render_device(self, camera: CameraDesc, out_ptr: int, stream_ptr: int | None = None,
                       depth: int = RT_DEFAULT_MAX_DEPTH, precision: str = "f32", out_format: str = "real",
                       shard=(0, 1), flags: int = 0) -> None:
         """Asynchronous render into a device buffer (e.g. a torch tensor's data_ptr()) on a HIP stream
         (stream_ptr None/0 = HIP's default stream, which is torch's default stream)."""
         opts = self.options(depth, precision, out_format, shard, flags)
-        _check(_lib.rt_render_device(self._h, C.byref(camera), C.byref(opts), C.c_void_p(out_ptr),
+        _check(_lib.rt_render_device(self._h, C.byref(camera), C.byref(opts), C.c_void_p(out_ptr or 0),
                                      C.c_void_p(stream_ptr or 0)))
 
     def color_at(self, rays, depth: int = RT_DEFAULT_MAX_DEPTH, precision: str = "f32"):
@@ -367,6 +445,23 @@ class Context:
         _check(_lib.rt_debug_tile_costs(self._h, None, 0, C.byref(n)))
         out = np.zeros(n.value, dtype=np.uint32)
         _check(_lib.rt_debug_tile_costs(self._h, out.ctypes.data_as(C.POINTER(C.c_uint32)), n.value, C.byref(n)))
+        return out
+
+    def debug_intersect(self, shape: int, rays, precision: str = "f64", world_space: bool = False):
+        """The device's per-shape intersect on (n, 6) rays: list of t tuples (push order) per ray."""
+        r = np.ascontiguousarray(np.asarray(rays, dtype=np.float64).reshape(-1, 6))
+        out = np.zeros((r.shape[0], 5), dtype=np.float64)
+        _check(_lib.rt_debug_intersect(self._h, shape, r.ctypes.data_as(C.POINTER(C.c_double)), r.shape[0],
+                                       PRECISIONS[precision], int(world_space),
+                                       out.ctypes.data_as(C.POINTER(C.c_double))))
+        return [tuple(row[1:1 + int(row[0])]) for row in out]
+
+    def debug_normal(self, shape: int, points, precision: str = "f64", world_space: bool = False) -> np.ndarray:
+        """The device's local_normal_at (world_space=False) or normal_at on (n, 3) points."""
+        p = np.ascontiguousarray(np.asarray(points, dtype=np.float64).reshape(-1, 3))
+        out = np.zeros_like(p)
+        _check(_lib.rt_debug_normal(self._h, shape, p.ctypes.data_as(C.POINTER(C.c_double)), p.shape[0],
+                                    PRECISIONS[precision], int(world_space), out.ctypes.data_as(C.POINTER(C.c_double))))
         return out
 
     def counters(self) -> dict:

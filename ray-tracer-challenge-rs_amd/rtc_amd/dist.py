@@ -1,21 +1,24 @@
 """Multi-GPU plumbing of the render path.
 
 Pixels are independent (camera.rs:106-110: every pixel is its own
-`color_at`), so the path shards without any data exchange:
+`color_at`), so a frame splits into shards with one data exchange at the end:
 
-* frames mode: each rank renders whole frames; a job's throughput is the
-  rays of all ranks over the slowest rank's time (`job_totals`).  No
-  collective touches the data path.
-* tiled mode: ONE frame is split into cyclic RT_TILE_H-row blocks (block t
-  belongs to shard t % N, balancing rows of very different cost).  Shard s
-  renders its blocks, in order, into a contiguous strip of `strip_height`
-  rows (the last block may be clipped; strips are padded to equal height so
-  the gather has one send count), the strips are gathered to rank 0
-  (`gather_strips`, RCCL on GPUs / gloo in the CPU tests) and rank 0
-  de-interleaves them (`rt_assemble_shards` on the device; `assemble_host`
-  is its host mirror for tests).
+* tiled (the north star's split, the library's own multi-GPU contexts,
+  csrc/rtc_group.cpp): ONE frame is split into cyclic RT_TILE_H-row blocks
+  (block t belongs to shard t % N, balancing rows of very different cost).
+  Shard s renders its blocks, in order, into a contiguous strip of
+  `strip_height` rows (strips are padded to equal height so the gather has one
+  send count); librtc RCCL-gathers the strips to rank 0, which de-interleaves
+  them on the device (rt_assemble_shards; `assemble_host` is its host mirror
+  for tests).  The world is flattened on rank 0 and RCCL-broadcast by
+  rt_scene_upload; this module only shares the communicator's unique id
+  (`share_unique_id`) and the camera over the control-plane process group.
+* frames (opt-in, weak scaling): each rank renders whole frames; a job's
+  throughput is the rays of all ranks over the slowest rank's time
+  (`job_totals`).  No collective touches the data path.
 
-The scene needs no broadcast: it is a few KB every rank loads itself.
+`gather_strips` / `broadcast_scene` are the same exchanges written with
+torch.distributed; the gloo tests (tests/test_dist.py) run them on CPU.
 """
 from __future__ import annotations
 
@@ -129,3 +132,24 @@ def job_totals(elapsed_s: float, rays: float, device) -> tuple[float, float]:
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dist.all_reduce(r, op=dist.ReduceOp.SUM)
     return float(t.item()), float(r.item())
+
+
+def share_unique_id(rank: int, src: int = 0) -> bytes:
+    """The RCCL unique id of a librtc group (rt_comm_unique_id on `src`),
+    sent to every rank over the initialised torch.distributed process group."""
+    import torch.distributed as dist
+
+    from . import comm_unique_id
+    box = [comm_unique_id() if rank == src else None]
+    dist.broadcast_object_list(box, src=src)
+    return box[0]
+
+
+def share_camera(camera, rank: int, src: int = 0):
+    """The camera `src` holds, as raw bytes (bit-exact), to every rank."""
+    import torch.distributed as dist
+
+    from . import CameraDesc
+    box = [bytes(camera) if rank == src else None]
+    dist.broadcast_object_list(box, src=src)
+    return CameraDesc.from_buffer_copy(box[0])

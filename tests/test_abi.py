@@ -42,7 +42,7 @@ def test_python_mirror_lists_every_symbol(rtc):
 
 
 def test_abi_version_and_last_error(rtc):
-    assert rtc.abi_version() == 1
+    assert rtc.abi_version() == rtc.RT_ABI_VERSION == 2
     lib = C.CDLL(LIB)
     lib.rt_last_error.restype = C.c_char_p
     assert lib.rt_last_error() is not None
@@ -53,6 +53,18 @@ def test_null_arguments_are_rejected():
     assert lib.rt_device_count(None) == RT_ERR_INVALID
     assert lib.rt_context_create(0, None) == RT_ERR_INVALID
     assert lib.rt_shard_rows(1080, 0, None) == RT_ERR_INVALID
+    assert lib.rt_shard_row_map(1080, 0, None, None) == RT_ERR_INVALID
+    assert lib.rt_context_create_multi(None, 1, None) == RT_ERR_INVALID
+    assert lib.rt_comm_unique_id(None) == RT_ERR_INVALID
+    assert lib.rt_context_create_rank(0, 2, 5, None, None) == RT_ERR_INVALID
+
+
+def test_no_device_means_no_multi_gpu_context(rtc):
+    if rtc.device_count() > 0:
+        pytest.skip("a HIP device is visible here")
+    with pytest.raises(rtc.RenderError) as e:
+        rtc.Context.multi([0])
+    assert e.value.code == RT_ERR_NO_DEVICE
 
 
 def test_no_device_means_an_error_not_a_fallback(rtc):

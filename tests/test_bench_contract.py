@@ -45,3 +45,25 @@ def test_bench_line_contract():
     assert abs(rl["frac"] - rl["achieved"] / rl["peak"]) < 1e-12
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_tiled_line_on_one_gpu():
+    """--mode tiled through librtc's RCCL group with one rank (the driver's
+    N > 1 default, scaled down): per-shard render, gather and end-to-end
+    milliseconds and the same workload on one GPU are reported."""
+    d = _run("--mode", "tiled", "--steps", "10", "--warmup", "2", "--width", "640", "--height", "360",
+             "--no-cpu-baseline")
+    assert KEYS <= set(d)
+    assert d["scaling"] == "strong" and d["config"]["mode"] == "tiled" and d["config"]["scene"] == "cover"
+    assert d["config"]["out"] == "u8" and d["config"]["parallelism"] == "tilesx1"
+    for k in ("render_ms_per_shard", "gather_ms", "frame_ms", "single_gpu_ms_per_step", "speedup_vs_1gpu"):
+        assert d[k] > 0, k
+    assert d["roofline"]["bound"] == "valu"
+
+
+@pytest.mark.gpu
+def test_bench_pool_scene_reports_cold_launch():
+    d = _run("--scene", "reflect_refract", "--steps", "10", "--warmup", "2", "--width", "320", "--height", "240",
+             "--no-cpu-baseline")
+    assert d["cold_kernel_ms"] > 0 and d["host_frame_ms"] > 0

@@ -134,3 +134,32 @@ def test_broadcast_scene_from_rank0(tmp_path):
     ref = rdist.scene_to_bytes(scene_fixture("cover"))
     for r in range(world):
         assert open(f"{out}.{r}", "rb").read() == ref
+
+
+def _camera_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    import rtc_amd
+    from rtc_amd import dist as rdist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cam = rtc_amd.camera_resize(scene_fixture("cover").camera, 3840, 2160) if rank == 0 else None
+        got = rdist.share_camera(cam, rank)
+        with open(f"{out_path}.{rank}", "wb") as f:
+            f.write(bytes(got))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_camera_reaches_every_rank_bit_exact(tmp_path, rtc):
+    """bench.py's tiled mode: the world stays on rank 0 (librtc broadcasts it),
+    the camera goes to the other ranks over the control-plane group, raw."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "cam")
+    mp.spawn(_camera_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    ref = bytes(rtc.camera_resize(scene_fixture("cover").camera, 3840, 2160))
+    for r in range(2):
+        assert open(f"{out}.{r}", "rb").read() == ref

@@ -1,0 +1,73 @@
+"""Multi-GPU contexts of the C-ABI (rtc_group.cpp) on the one-GPU test box.
+
+The RCCL path — the scene broadcast inside rt_scene_upload, the shard
+render into a strip, ncclGather onto rank 0 and the de-interleave — runs
+here with one rank, both as a one-process group (rt_context_create_multi,
+ncclCommInitAll) and as a rank of a one-process-per-GPU group
+(rt_context_create_rank, ncclCommInitRank).  Its frames must equal the
+single-GPU context's bit for bit, counters included.  The N-rank row-block
+math is pinned on CPU (tests/test_shards.py) and the 8-shard split on one
+device against the single-shot frame (tests/test_gpu_fullsize.py).
+"""
+import numpy as np
+import pytest
+
+from conftest import scene_fixture
+
+pytestmark = pytest.mark.gpu
+
+
+def _counts(st):
+    return {k: st[k] for k in ("primary", "shadow", "reflect", "refract", "shaded", "lit_patterned",
+                               "refract_evals", "schlick_evals")}
+
+
+@pytest.fixture(params=["multi", "rank"])
+def group_ctx(request, rtc):
+    if request.param == "multi":
+        ctx = rtc.Context.multi([0])
+    else:
+        ctx = rtc.Context.rank(0, 1, 0, rtc.comm_unique_id())
+    yield ctx
+    ctx.close()
+
+
+@pytest.mark.parametrize("name", ["cover", "three_sphere_scene", "reflect_refract"])
+def test_group_frames_equal_single_gpu(gpu_ctx, group_ctx, rtc, name):
+    scene = scene_fixture(name)
+    cam = rtc.camera_resize(scene.camera, 480, 270)
+    assert group_ctx.group() == (1, 0, 1)
+    group_ctx.upload(scene)
+    gpu_ctx.upload(scene)
+    for precision, fmt in (("f32", "real"), ("f64", "real"), ("f32", "u8")):
+        a, sa = gpu_ctx.render(cam, 6, precision=precision, out_format=fmt)
+        b, sb = group_ctx.render(cam, 6, precision=precision, out_format=fmt)
+        assert np.array_equal(a, b), (name, precision, fmt)
+        assert _counts(sa) == _counts(sb)
+        assert sb["n_shards"] == 1 and sb["frame_ms"] >= sb["kernel_ms"] > 0 and sb["gather_ms"] >= 0
+
+
+def test_group_render_device_and_options(gpu_ctx, group_ctx, rtc):
+    import torch
+    scene = scene_fixture("table")
+    cam = rtc.camera_resize(scene.camera, 333, 201)  # ragged last tile row
+    group_ctx.upload(scene)
+    gpu_ctx.upload(scene)
+    ref, _ = gpu_ctx.render(cam, 6, precision="f32")
+    out = torch.zeros((cam.height, cam.width, 3), dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):  # repeated frames: cost-ordered pool launches, reused strips
+        group_ctx.render_device(cam, out.data_ptr(), s, 6, "f32")
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
+    with pytest.raises(rtc.RenderError):  # the group shards frames itself
+        group_ctx.render(cam, 6, precision="f32", shard=(0, 2))
+
+
+def test_group_upload_errors_are_reported(group_ctx, rtc):
+    bad = scene_fixture("cover")
+    bad.shapes[0].material = 999
+    with pytest.raises(rtc.RenderError):
+        group_ctx.upload(bad)
+    with pytest.raises(rtc.RenderError):  # nothing uploaded yet
+        group_ctx.render(rtc.camera_resize(bad.camera, 8, 8), 6)

@@ -1,0 +1,267 @@
+"""The reference's own per-shape and camera known answers, run on the GPU.
+
+The oracle passes these (tests/test_oracle_kat.py); here the PRODUCT's device
+code is checked against the same expected values (tests/golden/
+reference_kats.json, transcribed from the reference's unit tests):
+
+  * per-shape intersections and normals through rt_debug_intersect /
+    rt_debug_normal, which run the kernels' own `entries<>` / `normal_at`
+    device functions (csrc/rtc_kernels.hip) on the reference's test rays;
+  * the camera: rt_camera_make / rt_camera_set_transform (host f64) and the
+    device's ray_for_pixel (camera_ray) read back through RT_FLAG_NO_TRACE
+    (output colour = ray direction), camera.rs:172-249.
+
+f64 must equal the reference's exact values where the reference asserts
+assert_eq! and agree within EPSILON = 8e-8 where it uses coarse_eq; f32
+agrees within F32_TOL with the same entry counts.  Inputs are the reference
+tests' own (file named per case); directions the reference normalises are
+normalised with its formula (vector.rs:84-91: each component / sqrt of the
+sum of squares).
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+EPSILON = 8e-8
+F32_TOL = 2e-5
+F64_MAX = 1.7976931348623157e308
+GOLD = json.load(open(os.path.join(GOLDEN, "reference_kats.json")))["cases"]
+
+
+def _norm(v):
+    m = math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])
+    return (v[0] / m, v[1] / m, v[2] / m)
+
+
+def _ray(o, d, normalize=False):
+    return tuple(o) + (_norm(d) if normalize else tuple(map(float, d)))
+
+
+T3 = math.sqrt(3.0) / 3.0
+S2 = math.sqrt(2.0)
+
+
+def _shapes():
+    from rtc_amd import world as W
+    inf = F64_MAX
+    return {
+        "sphere": W.sphere(),
+        "sphere_scaled": W.sphere(transform=W.scaling(2, 2, 2)),
+        "sphere_translated": W.sphere(transform=W.translation(5, 0, 0)),
+        "sphere_up": W.sphere(transform=W.translation(0, 1, 0)),
+        "sphere_transformed": W.sphere(transform=W.mat_mul(W.scaling(1, 0.5, 1), W.rotation_z(math.pi / 5.0))),
+        "plane": W.plane(),
+        "cube": W.cube(),
+        "cylinder": W.cylinder(-inf, inf, False),
+        "cylinder_1_2": W.cylinder(1.0, 2.0, False),
+        "cylinder_1_2_closed": W.cylinder(1.0, 2.0, True),
+        "cone": W.cone(-inf, inf, False),
+        "cone_caps": W.cone(-0.5, 0.5, True),
+        "triangle": W.triangle((0, 1, 0), (-1, 0, 0), (1, 0, 0)),
+    }
+
+
+# (golden case, shape, rays, world_space, layout)  layout: "ts" = the t list of
+# one ray, "count+ts" = per ray count then ts, "counts" = per ray count
+INTERSECT_CASES = [
+    ("ray.sphere_middle", "sphere", [_ray((0, 0, -5), (0, 0, 1))], True, "ts"),
+    ("ray.sphere_tangent", "sphere", [_ray((0, 1, -5), (0, 0, 1))], True, "ts"),
+    ("ray.sphere_miss", "sphere", [_ray((0, 2, -5), (0, 0, 1))], True, "ts"),
+    ("ray.sphere_inside", "sphere", [_ray((0, 0, 0), (0, 0, 1))], True, "ts"),
+    ("ray.sphere_behind", "sphere", [_ray((0, 0, 5), (0, 0, 1))], True, "ts"),
+    ("ray.sphere_scaled", "sphere_scaled", [_ray((0, 0, -5), (0, 0, 1))], True, "ts"),
+    ("ray.sphere_translated", "sphere_translated", [_ray((0, 0, -5), (0, 0, 1))], True, "ts"),
+    ("plane.parallel", "plane", [_ray((0, 10, 0), (0, 0, 1))], False, "ts"),
+    ("plane.from_above", "plane", [_ray((0, 1, 0), (0, -1, 0))], False, "ts"),
+    ("plane.from_below", "plane", [_ray((0, -1, 0), (0, 1, 0))], False, "ts"),
+    ("cube.ray_intersects", "cube",  # cube.rs ray_intersects_cube
+     [_ray(o, d) for o, d in [((5, 0.5, 0), (-1, 0, 0)), ((-5, 0.5, 0), (1, 0, 0)), ((0.5, 5, 0), (0, -1, 0)),
+                              ((0.5, -5, 0), (0, 1, 0)), ((0.5, 0, 5), (0, 0, -1)), ((0.5, 0, -5), (0, 0, 1)),
+                              ((0, 0.5, 0), (0, 0, 1))]], False, "count+ts"),
+    ("cube.ray_misses_counts", "cube",  # cube.rs ray_misses_cube
+     [_ray(o, d) for o, d in [((-2, 0, 0), (0.2673, 0.5345, 0.8018)), ((0, -2, 0), (0.8018, 0.2673, 0.5345)),
+                              ((0, 0, -2), (0.5345, 0.8018, 0.2673)), ((2, 0, 2), (0, 0, -1)),
+                              ((0, 2, 2), (0, -1, 0)), ((2, 2, 0), (-1, 0, 0)), ((0, 0, 2), (0, 0, 1))]],
+     False, "counts"),
+    ("cylinder.misses_counts", "cylinder",  # cylinder.rs ray_misses_cylinder
+     [_ray(o, d, True) for o, d in [((1, 0, 0), (0, 1, 0)), ((0, 1, 0), (0, 1, 0)), ((0, 0, -5), (1, 1, 1))]],
+     False, "counts"),
+    ("cylinder.intersects", "cylinder",  # cylinder.rs ray_intersects_cylinder
+     [_ray(o, d, True) for o, d in [((1, 0, -5), (0, 0, 1)), ((0, 0, -5), (0, 0, 1)), ((0.5, 0, -5), (0.1, 1, 1))]],
+     False, "count+ts"),
+    ("cylinder.constrained_counts", "cylinder_1_2",  # cylinder.rs intersecting_constrained_cylinder
+     [_ray(o, d, True) for o, d in [((0, 1.5, 0), (0.1, 1, 0)), ((0, 3, -5), (0, 0, 1)), ((0, 0, -5), (0, 0, 1)),
+                                    ((0, 2, -5), (0, 0, 1)), ((0, 1, -5), (0, 0, 1)), ((0, 1.5, -2), (0, 0, 1))]],
+     False, "counts"),
+    ("cylinder.caps_counts", "cylinder_1_2_closed",  # cylinder.rs intersecting_caps_of_closed_cylinder
+     [_ray(o, d, True) for o, d in [((0, 3, 0), (0, -1, 0)), ((0, 3, -2), (0, -1, 2)), ((0, 4, -2), (0, -1, 1)),
+                                    ((0, 0, -2), (0, 1, 2)), ((0, -1, -2), (0, 1, 1))]], False, "counts"),
+    ("cone.intersects", "cone",  # cone.rs intersecting_ray_with_cone
+     [_ray(o, d, True) for o, d in [((0, 0, -5), (0, 0, 1)), ((0, 0, -5), (1, 1, 1)), ((1, 1, -5), (-0.5, -1, 1))]],
+     False, "count+ts"),
+    ("cone.parallel_to_half", "cone", [_ray((0, 0, -1), (0, 1, 1), True)], False, "ts"),  # single-root branch
+    ("cone.caps_counts", "cone_caps",  # cone.rs intersecting_ray_with_cone_caps
+     [_ray(o, d, True) for o, d in [((0, 0, -5), (0, 1, 0)), ((0, 0, -0.25), (0, 1, 1)), ((0, 0, -0.25), (0, 1, 0))]],
+     False, "counts"),
+    ("triangle.misses_counts", "triangle",  # triangle.rs ray_parallel_to_triangle / ray_misses_*_edge
+     [_ray(o, d) for o, d in [((0, -1, -2), (0, 1, 0)), ((1, 1, -2), (0, 0, 1)), ((-1, 1, -2), (0, 0, 1)),
+                              ((0, -1, -2), (0, 0, 1))]], False, "counts"),
+    ("triangle.intersects", "triangle", [_ray((0, 0.5, -2), (0, 0, 1))], False, "ts"),
+]
+
+NORMAL_CASES = [
+    ("sphere.normals", "sphere", [(1, 0, 0), (0, 1, 0), (0, 0, 1), (T3, T3, T3)], True),
+    ("sphere.normal_translated", "sphere_up", [(0.0, 1.0 + math.sqrt(0.5), -math.sqrt(0.5))], True),
+    ("sphere.normal_transformed", "sphere_transformed", [(0, S2 / 2.0, -S2 / 2.0)], True),
+    ("plane.normal_is_constant", "plane", [(0, 0, 0), (10, 0, -10), (-5, 0, 150)], True),
+    ("cube.normals", "cube", [(1, 0.5, -0.8), (-1, -0.2, 0.9), (-0.4, 1, -0.1), (0.3, -1, -0.7), (-0.6, 0.3, 1),
+                              (0.4, 0.4, -1), (1, 1, 1), (-1, -1, -1)], False),
+    ("cylinder.normals", "cylinder", [(1, 0, 0), (0, 5, -1), (0, -2, 1), (-1, 1, 0)], False),
+    ("cylinder.cap_normals", "cylinder_1_2_closed", [(0, 1, 0), (0.5, 1, 0), (0, 1, 0.5), (0, 2, 0), (0.5, 2, 0),
+                                                     (0, 2, 0.5)], False),
+    ("cone.normals", "cone", [(0, 0, 0), (1, 1, 1), (-1, -1, 0)], False),
+    ("triangle.normal", "triangle", [(0, 0.5, 0)], False),
+]
+
+
+@pytest.fixture(scope="module")
+def kat_world(gpu_ctx):
+    from rtc_amd import world as W
+    shapes = _shapes()
+    names = list(shapes)
+    gpu_ctx.upload(W.World([W.Light((-10, 10, -10))], [shapes[n] for n in names]).tables())
+    return {n: i for i, n in enumerate(names)}
+
+
+def _flatten(layout, per_ray):
+    if layout == "ts":
+        assert len(per_ray) == 1
+        return list(per_ray[0])
+    if layout == "counts":
+        return [float(len(t)) for t in per_ray]
+    out = []
+    for t in per_ray:
+        out += [float(len(t))] + list(t)
+    return out
+
+
+def _close(got, exp, mode, precision):
+    assert len(got) == len(exp), (got, exp)
+    for g, e in zip(got, exp):
+        if precision == "f32":
+            assert abs(g - e) <= F32_TOL * max(1.0, abs(e)), (got, exp)
+        elif mode == "exact":
+            assert g == e, (got, exp)
+        else:
+            assert g == e or abs(g - e) < EPSILON, (got, exp)
+
+
+# f32 cannot resolve these rays: cone.rs's second case grazes the cone, its two
+# f64 roots 8.660254015492644 and 8.660254060196127 differ by 5e-9 relative
+# (below the f32 ulp), so the f32 discriminant may round below zero (no entry)
+# or keep both.  The f64 path must match exactly; f32 may drop the pair.
+F32_GRAZING = {("cone.intersects", 1)}
+
+
+def _expected_per_ray(layout, exp, n):
+    if layout != "count+ts":
+        return None
+    out, i = [], 0
+    for _ in range(n):
+        c = int(exp[i])
+        out.append(list(exp[i + 1:i + 1 + c]))
+        i += 1 + c
+    return out
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("case", INTERSECT_CASES, ids=[c[0] for c in INTERSECT_CASES])
+def test_device_intersections_match_reference(gpu_ctx, kat_world, case, precision):
+    name, shape, rays, world_space, layout = case
+    got = gpu_ctx.debug_intersect(kat_world[shape], rays, precision=precision, world_space=world_space)
+    exp = GOLD[name]["expected"]
+    grazing = [i for (n, i) in F32_GRAZING if n == name] if precision == "f32" else []
+    if grazing:
+        per = _expected_per_ray(layout, exp, len(rays))
+        for i in grazing:
+            assert len(got[i]) in (0, len(per[i])), (got[i], per[i])
+            if got[i]:
+                _close(list(got[i]), per[i], "coarse", precision)
+        keep = [i for i in range(len(rays)) if i not in grazing]
+        got = [got[i] for i in keep]
+        exp = [v for i in keep for v in [float(len(per[i]))] + per[i]]
+    _close(_flatten(layout, got), exp, GOLD[name]["mode"], precision)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("case", NORMAL_CASES, ids=[c[0] for c in NORMAL_CASES])
+def test_device_normals_match_reference(gpu_ctx, kat_world, case, precision):
+    name, shape, points, world_space = case
+    got = gpu_ctx.debug_normal(kat_world[shape], points, precision=precision, world_space=world_space)
+    _close([float(v) for v in got.reshape(-1)], GOLD[name]["expected"], GOLD[name]["mode"], precision)
+
+
+def test_device_intersect_f32_agrees_with_f64_on_random_rays(gpu_ctx, kat_world):
+    """Beyond the fixed cases: every shape of the KAT world on 2048 random
+    world rays; the f32 path pushes the same number of entries as the f64
+    path (pinned above) except for rays grazing an edge or silhouette."""
+    rng = np.random.default_rng(11)
+    o = rng.uniform(-4, 4, size=(2048, 3))
+    d = rng.normal(size=(2048, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([o, d], axis=1)
+    for shape, idx in kat_world.items():
+        a = gpu_ctx.debug_intersect(idx, rays, precision="f64", world_space=True)
+        b = gpu_ctx.debug_intersect(idx, rays, precision="f32", world_space=True)
+        agree = sum(len(x) == len(y) for x, y in zip(a, b)) / len(a)
+        assert agree > 0.99, shape  # f32 flips only rays grazing an edge
+
+
+# ------------------------------------------------------------------ camera
+def _no_trace_directions(gpu_ctx, cam):
+    """Device ray_for_pixel for every pixel: RT_FLAG_NO_TRACE stores the
+    primary direction as the pixel colour (f64 output)."""
+    import ctypes as C
+
+    from rtc_amd import RT_FLAG_NO_TRACE, Stats, _check, _lib
+    opts = gpu_ctx.options(6, "f64", "real", (0, 1), RT_FLAG_NO_TRACE)
+    img = np.zeros((cam.height, cam.width, 3), dtype=np.float64)
+    _check(_lib.rt_render(gpu_ctx._h, C.byref(cam), C.byref(opts), img.ctypes.data_as(C.c_void_p),
+                          C.byref(Stats())))
+    return img
+
+
+def test_device_camera_rays_match_reference(gpu_ctx, rtc):
+    from rtc_amd import world as W
+    gpu_ctx.upload(W.World.default().tables())
+    cam = rtc.camera_set_transform(rtc.camera_make(201, 101, math.pi / 2, (0, 0, 0), (0, 0, -1), (0, 1, 0)),
+                                   W.IDENTITY)
+    img = _no_trace_directions(gpu_ctx, cam)
+    # camera.rs:192-201 ray_through_canvas_corner (assert_eq!)
+    assert tuple(img[0, 0]) == tuple(GOLD["camera.ray_through_corner"]["expected"][3:])
+    # camera.rs:184-190 ray_through_canvas_center (coarse_eq)
+    assert np.abs(img[50, 100] - np.array([0.0, 0.0, -1.0])).max() < EPSILON
+    # camera.rs:203-213 ray_through_canvas_with_transformed_camera
+    t = rtc.camera_set_transform(cam, W.mat_mul(W.rotation_y(math.pi / 4.0), W.translation(0, -2, 5)))
+    assert tuple(t.origin) == (0.0, 2.0, -5.0)
+    img = _no_trace_directions(gpu_ctx, t)
+    assert np.abs(img[50, 100] - np.array([S2 / 2.0, 0.0, -S2 / 2.0])).max() < EPSILON
+
+
+def test_device_render_default_world_pixel(gpu_ctx, rtc):
+    """camera.rs:215-249: World::default through an 11x11 camera, pixel (5, 5)."""
+    from rtc_amd import world as W
+    gpu_ctx.upload(W.World.default().tables())
+    cam = rtc.camera_make(11, 11, math.pi / 2, (0, 0, -5), (0, 0, 0), (0, 1, 0))
+    exp = np.array(GOLD["camera.render_default_world"]["expected"])
+    img, _ = gpu_ctx.render(cam, 6, precision="f64")
+    assert np.abs(img[5, 5] - exp).max() < EPSILON
+    img32, _ = gpu_ctx.render(cam, 6, precision="f32")
+    assert np.abs(img32[5, 5] - exp).max() < 1e-5

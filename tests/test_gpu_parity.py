@@ -362,8 +362,9 @@ def test_consecutive_launches_keep_queue_epochs(gpu_ctx, rtc):
     the same frames and counters exactly."""
     scene = scene_fixture("reflect_refract")
     gpu_ctx.upload(scene)
-    # 1920x1080 has more tiles than resident workgroups: the direct kernel runs
-    # static rounds, then its queues (hybrid); the small ones are all-queue
+    # 1920x1080 has more tiles than resident workgroups (the direct kernel's
+    # static stride runs several rounds, the pool kernel's queues hand out
+    # tiles by atomics); the small canvases fit in one round
     cams = [rtc.camera_resize(scene.camera, w, h)
             for (w, h) in ((37, 29), (1920, 1080), (200, 100), (16, 16), (1000, 700), (1, 7))]
     first = {}
