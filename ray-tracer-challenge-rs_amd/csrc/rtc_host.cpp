@@ -27,13 +27,15 @@
 namespace rtc {
 
 template <typename R>
-hipError_t launch_trace(const LaunchParams<R>& P, bool pool, uint32_t grid, size_t dyn_lds, hipStream_t stream);
+hipError_t launch_trace(const LaunchParams<R>& P, bool pool, bool dup, uint32_t grid, size_t dyn_lds,
+                        hipStream_t stream);
 template <typename R>
 hipError_t occupancy(bool pool, bool lds, size_t dyn_lds, int* blocks_per_cu);
 
 namespace sp {  // rtc_kernels_sp.o: the f32 pool kernel for worlds of spheres and planes only
 template <typename R>
-hipError_t launch_trace(const LaunchParams<R>& P, bool pool, uint32_t grid, size_t dyn_lds, hipStream_t stream);
+hipError_t launch_trace(const LaunchParams<R>& P, bool pool, bool dup, uint32_t grid, size_t dyn_lds,
+                        hipStream_t stream);
 }  // namespace sp
 constexpr uint32_t kKindsSp = (1u << RT_SHAPE_SPHERE) | (1u << RT_SHAPE_PLANE);
 
@@ -519,9 +521,12 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     uint32_t kinds = 0;
     for (int k = 0; k < kNumKinds; ++k)
         if (w.scene.kind_begin[k + 1] > w.scene.kind_begin[k]) kinds |= 1u << k;
-    const bool sp = sizeof(R) == 4 && ls.pool && ctx->kind_variants && (kinds & ~kKindsSp) == 0;
-    if (hipError_t e = sp ? sp::launch_trace<R>(P, ls.pool, ls.grid, ls.lds, stream)
-                          : launch_trace<R>(P, ls.pool, ls.grid, ls.lds, stream);
+    // value-equal shapes (rt_scene_upload's identity classes) take the pool
+    // kernel whose containers walk aggregates per class
+    const bool dup = ctx->duplicate_shapes > 0;
+    const bool sp = sizeof(R) == 4 && ls.pool && ctx->kind_variants && (kinds & ~kKindsSp) == 0 && !dup;
+    if (hipError_t e = sp ? sp::launch_trace<R>(P, ls.pool, dup, ls.grid, ls.lds, stream)
+                          : launch_trace<R>(P, ls.pool, dup, ls.grid, ls.lds, stream);
         e != hipSuccess)
         return set_error(RT_ERR_HIP, std::string("launch of the ") + (ls.pool ? "pool" : "direct") + " kernel (grid " +
                                          std::to_string(ls.grid) + ", dynamic LDS " + std::to_string(ls.lds) +
