@@ -774,7 +774,9 @@ __device__ inline V3<R> lighting_term(const LightRec<R>& L, const MaterialRec<R>
         if (!(ldn < (R)0)) {
             c = {c.x + (eff.x * m.diffuse) * ldn, c.y + (eff.y * m.diffuse) * ldn, c.z + (eff.z * m.diffuse) * ldn};
             const R rde = dot(reflect(vneg(ld), n), eye);
-            if (!(rde <= (R)0)) {
+            // specular 0 (every wall of three_sphere) adds exactly +0: skip the
+            // pow (two transcendentals) for those lanes
+            if (!(rde <= (R)0) && m.specular != (R)0) {
                 const R f = Real<R>::pow(rde, m.shininess);
                 c = {c.x + (L.intensity[0] * m.specular) * f, c.y + (L.intensity[1] * m.specular) * f,
                      c.z + (L.intensity[2] * m.specular) * f};
@@ -901,12 +903,19 @@ __device__ inline void store_pixel(const LaunchParams<R>& P, uint64_t idx, V3<R>
 }
 
 // Tile t of this launch -> pixel of thread `tid` (x, y, output index).
+#ifndef RTC_WAVE_W
+#define RTC_WAVE_W 16  // a wave's pixel block: 16 x 4 (64: one 64-pixel row)
+#endif
+static_assert(RT_TILE_W % RTC_WAVE_W == 0 && RT_TILE_H % (64 / RTC_WAVE_W) == 0, "the 4 waves tile the tile");
 template <typename R>
 __device__ inline bool tile_pixel(const LaunchParams<R>& P, uint32_t t, uint32_t tid, uint32_t& x, uint32_t& y,
                                   uint64_t& out_idx) {
     const uint32_t lrow = t / P.tiles_x, tcol = t - lrow * P.tiles_x;
-    const uint32_t local_y = lrow * RT_TILE_H + (tid / RT_TILE_W);  // row in this shard's strip
-    x = tcol * RT_TILE_W + (tid % RT_TILE_W);
+    // wave w of the tile covers one RTC_WAVE_W x (64 / RTC_WAVE_W) pixel block
+    constexpr uint32_t kPerRow = RT_TILE_W / RTC_WAVE_W, kWaveH = 64 / RTC_WAVE_W;
+    const uint32_t wave = tid / 64, lane = tid % 64;
+    const uint32_t local_y = lrow * RT_TILE_H + (wave / kPerRow) * kWaveH + lane / RTC_WAVE_W;  // row in the strip
+    x = tcol * RT_TILE_W + (wave % kPerRow) * RTC_WAVE_W + lane % RTC_WAVE_W;
     y = shard_image_row(local_y, P.shard_count, P.shard_index);
     out_idx = (uint64_t)local_y * P.width + x;
     return x < P.width && y < P.height;
