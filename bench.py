@@ -298,11 +298,14 @@ def main():
                     cold.append(timed_launches(step, stream, 1))
                 line["cold_kernel_ms"] = float(np.median(cold))
             # a drop-in Camera::render: synchronous rt_render into host memory,
-            # PCIe copy included (median of 10; never `value`)
+            # PCIe copy included, into a canvas kept across frames (median of
+            # 10; never `value`).  A canvas allocated per call adds its first-
+            # touch page faults (~0.3 ms at 1080p f32; scripts/host_frame_probe.py).
+            canvas, _ = ctx.render(cam, args.depth, args.precision, args.out)
             lat = []
             for _ in range(10):
                 t = time.perf_counter()
-                ctx.render(cam, args.depth, args.precision, args.out)
+                ctx.render(cam, args.depth, args.precision, args.out, out=canvas)
                 lat.append((time.perf_counter() - t) * 1e3)
             line["host_frame_ms"] = float(np.median(lat))
         if world == 1 and not args.no_cpu_baseline:

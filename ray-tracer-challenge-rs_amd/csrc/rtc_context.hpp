@@ -95,6 +95,9 @@ struct rt_context {
     uint32_t stamp_capacity = 0, stamp_count = 0;
     void* d_scratch = nullptr;  // host-buffer renders / color_at staging
     size_t scratch_bytes = 0;
+    // rt_render: counters before/after and the error flag come back pinned,
+    // on the stream, so a frame needs one host sync
+    unsigned long long* h_counters = nullptr;  // 2 x kCounterShards x kNumCounters + the error flag
     // Multi-GPU group (rtc_group.cpp).  A frame is split
     // into n_ranks shards of cyclic RT_TILE_H-row blocks; this member renders
     // shard `rank` into d_strip, RCCL gathers the strips onto rank 0, which
@@ -121,6 +124,9 @@ int read_counters(rt_context* ctx, unsigned long long out[kNumCounters]);
 void fill_stats(rt_context* ctx, const unsigned long long before[kNumCounters],
                 const unsigned long long after[kNumCounters], float ms, rt_stats* s);
 int check_pool_error(rt_context* ctx);
+int order_after_last(rt_context* ctx, hipStream_t stream);  // cross-stream launch order (rtc.h)
+int ensure_host_counters(rt_context* ctx);
+int copy_to_host(rt_context* ctx, void* out, size_t bytes);  // d_scratch -> caller host buffer, on ctx->stream
 uint32_t tile_rows_for(uint32_t height, uint32_t shards, uint32_t shard);
 int validate_scene(const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats, uint32_t nm,
                    const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights, uint32_t nl);

@@ -303,13 +303,13 @@ int group_render(rt_context* ctx, const rt_camera_desc* cam, const rt_render_opt
         if ((rc = ensure_scratch(ctx, bytes))) return rc;
     }
     if ((rc = render_shards(ctx, cam, o, ctx->rank == 0 ? ctx->d_scratch : nullptr, ctx->stream, true))) return rc;
+    if (ctx->rank == 0) {  // enqueued behind the de-interleave on rank 0's stream
+        RT_HIP(hipSetDevice(ctx->device));
+        if ((rc = copy_to_host(ctx, out_host, bytes))) return rc;
+    }
     for (rt_context* m : ms) {
         RT_HIP(hipSetDevice(m->device));
         RT_HIP(hipStreamSynchronize(m->stream));
-    }
-    if (ctx->rank == 0) {
-        RT_HIP(hipSetDevice(ctx->device));
-        RT_HIP(hipMemcpy(out_host, ctx->d_scratch, bytes, hipMemcpyDeviceToHost));
     }
     rt_stats total{};
     float render_ms = 0.f, gather_ms = 0.f, frame_ms = 0.f;

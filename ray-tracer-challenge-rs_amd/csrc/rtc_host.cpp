@@ -432,10 +432,21 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
     return RT_OK;
 }
 
+int order_after_last(rt_context* ctx, hipStream_t stream) {
+    if (ctx->launched && stream != ctx->last_stream) {
+        RT_HIP(hipEventRecord(ctx->ev_order, ctx->last_stream));
+        RT_HIP(hipStreamWaitEvent(stream, ctx->ev_order, 0));
+    }
+    ctx->last_stream = stream;
+    ctx->launched = true;
+    return RT_OK;
+}
+
 template <typename R>
 int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const double* d_rays, uint64_t n_rays,
            uint32_t depth, uint32_t out_format, uint32_t shard_index, uint32_t shard_count, void* out_device,
            hipStream_t stream, uint32_t flags = 0) {
+    int rc;
     LaunchParams<R> P{};
     P.scene = w.scene;
     if (cam) {
@@ -463,14 +474,9 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     P.counters = ctx->d_counters;
     P.error_flag = ctx->d_error;
     if (P.n_tiles == 0) return RT_OK;
-    if (ctx->launched && stream != ctx->last_stream) {
-        RT_HIP(hipEventRecord(ctx->ev_order, ctx->last_stream));
-        RT_HIP(hipStreamWaitEvent(stream, ctx->ev_order, 0));
-    }
-    ctx->last_stream = stream;
-    ctx->launched = true;
+    if ((rc = order_after_last(ctx, stream))) return rc;
     LaunchShape ls;
-    int rc = plan_launch<R>(ctx, w.scene, depth, P.n_tiles, ls);
+    rc = plan_launch<R>(ctx, w.scene, depth, P.n_tiles, ls);
     if (rc) return rc;
     P.pool_capacity = ls.cap;
     P.pool_lds_capacity = ls.lcap;
@@ -590,6 +596,25 @@ void fill_stats(rt_context* ctx, const unsigned long long before[kNumCounters],
     s->reserved = 0;
 }
 
+int ensure_host_counters(rt_context* ctx) {
+    if (ctx->h_counters) return RT_OK;
+    const size_t cbytes = 2 * (size_t)kCounterShards * kNumCounters * sizeof(unsigned long long) + 64;
+    RT_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_counters), cbytes, hipHostMallocDefault));
+    return RT_OK;
+}
+
+// Device scratch -> the caller's host buffer, enqueued on ctx->stream after
+// the render.  A pageable hipMemcpyAsync runs at the PCIe rate here (the
+// runtime pipelines its own pinned staging): measured on MI355X for a 1080p
+// f32 frame (24.9 MB) into a canvas kept across frames, 0.52 ms per whole
+// rt_render call; a pinned staging buffer copied out by 4 host threads as
+// each of 8 DMA chunks landed took 0.71 ms (scripts/host_frame_probe.py).
+// A canvas allocated per call pays its page faults on top (~0.3 ms at 1080p).
+int copy_to_host(rt_context* ctx, void* out, size_t bytes) {
+    RT_HIP(hipMemcpyAsync(out, ctx->d_scratch, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    return RT_OK;
+}
+
 int check_pool_error(rt_context* ctx) {
     int32_t err = 0;
     RT_HIP(hipMemcpy(&err, ctx->d_error, sizeof(err), hipMemcpyDeviceToHost));
@@ -701,6 +726,7 @@ void destroy_device_context(rt_context* ctx) {
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     (void)hipFree(ctx->d_strip);
     (void)hipFree(ctx->d_gathered);
+    if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
     for (hipEvent_t e : {ctx->ev_render0, ctx->ev_render1, ctx->ev_gather1})
         if (e) (void)hipEventDestroy(e);
     delete ctx;
@@ -798,24 +824,43 @@ int rt_render(rt_context* ctx, const rt_camera_desc* cam, const rt_render_option
     const uint32_t rows = tile_rows_for(cam->height, o->shard_count, o->shard_index) * RT_TILE_H;
     const uint32_t valid_rows = o->shard_count == 1 ? cam->height : rows;
     const size_t bytes = (size_t)rows * cam->width * 3 * elem;
+    const size_t out_bytes = (size_t)valid_rows * cam->width * 3 * elem;
     if (bytes == 0) {
         if (stats) std::memset(stats, 0, sizeof(*stats));
         return RT_OK;
     }
     if ((rc = ensure_scratch(ctx, bytes))) return rc;
-    RT_HIP(hipMemsetAsync(ctx->d_scratch, 0, bytes, ctx->stream));
-    unsigned long long before[kNumCounters], after[kNumCounters];
-    if ((rc = read_counters(ctx, before))) return rc;
-    RT_HIP(hipEventRecord(ctx->ev_start, ctx->stream));
-    if ((rc = rt_render_device(ctx, cam, o, ctx->d_scratch, static_cast<void*>(ctx->stream)))) return rc;
-    RT_HIP(hipEventRecord(ctx->ev_stop, ctx->stream));
-    RT_HIP(hipStreamSynchronize(ctx->stream));
+    if ((rc = ensure_host_counters(ctx))) return rc;
+    hipStream_t s = ctx->stream;
+    // counters before and after, and the error flag, come back in pinned
+    // memory on the stream: one host sync for the whole frame
+    if ((rc = order_after_last(ctx, s))) return rc;
+    const size_t cbytes = (size_t)kCounterShards * kNumCounters * sizeof(unsigned long long);
+    unsigned long long* h_before = ctx->h_counters;
+    unsigned long long* h_after = ctx->h_counters + (size_t)kCounterShards * kNumCounters;
+    int32_t* h_err = reinterpret_cast<int32_t*>(h_after + (size_t)kCounterShards * kNumCounters);
+    RT_HIP(hipMemcpyAsync(h_before, ctx->d_counters, cbytes, hipMemcpyDeviceToHost, s));
+    if (o->shard_count > 1) RT_HIP(hipMemsetAsync(ctx->d_scratch, 0, bytes, s));  // strip rows past the canvas
+    RT_HIP(hipEventRecord(ctx->ev_start, s));
+    if ((rc = launch_frame(ctx, cam, o, o->shard_index, o->shard_count, ctx->d_scratch, s))) return rc;
+    RT_HIP(hipEventRecord(ctx->ev_stop, s));
+    RT_HIP(hipMemcpyAsync(h_after, ctx->d_counters, cbytes, hipMemcpyDeviceToHost, s));
+    RT_HIP(hipMemcpyAsync(h_err, ctx->d_error, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if ((rc = copy_to_host(ctx, out_host, out_bytes))) return rc;
+    RT_HIP(hipStreamSynchronize(s));
     float ms = 0.f;
     RT_HIP(hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_stop));
-    RT_HIP(hipMemcpy(out_host, ctx->d_scratch, (size_t)valid_rows * cam->width * 3 * elem, hipMemcpyDeviceToHost));
-    if ((rc = check_pool_error(ctx))) return rc;
+    if (*h_err) {
+        RT_HIP(hipMemset(ctx->d_error, 0, sizeof(int32_t)));
+        return set_error(RT_ERR_POOL, "device ray pool overflow");
+    }
     if (stats) {
-        if ((rc = read_counters(ctx, after))) return rc;
+        unsigned long long before[kNumCounters] = {}, after[kNumCounters] = {};
+        for (int sh = 0; sh < kCounterShards; ++sh)
+            for (int i = 0; i < kNumCounters; ++i) {
+                before[i] += h_before[(size_t)sh * kNumCounters + i];
+                after[i] += h_after[(size_t)sh * kNumCounters + i];
+            }
         fill_stats(ctx, before, after, ms, stats);
     }
     return RT_OK;
@@ -885,10 +930,7 @@ int debug_shape(rt_context* ctx, uint32_t shape, uint32_t mode, const double* in
     RT_HIP(hipMemcpyAsync(d_in, in, in_bytes, hipMemcpyHostToDevice, ctx->stream));
     const int32_t ws = ctx->world_slot[shape];
     const int slot = ws & 0xFFFFFF, kind = ws >> 24;
-    if (ctx->launched && ctx->last_stream != ctx->stream) {  // scratch may be in use by nothing else, but keep order
-        RT_HIP(hipEventRecord(ctx->ev_order, ctx->last_stream));
-        RT_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_order, 0));
-    }
+    if ((rc = order_after_last(ctx, ctx->stream))) return rc;
     hipError_t e = precision == RT_PRECISION_F32
                        ? launch_debug_shape<float>(ctx->w32.shapes, slot, kind, mode, world_space, d_in, (uint32_t)n,
                                                    d_out, ctx->stream)

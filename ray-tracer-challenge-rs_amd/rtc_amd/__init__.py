@@ -393,12 +393,18 @@ class Context:
         return RenderOptions(depth, PRECISIONS[precision], OUT_FORMATS[out_format], shard[0], shard[1], flags)
 
     def render(self, camera: CameraDesc, depth: int = RT_DEFAULT_MAX_DEPTH, precision: str = "f32",
-               out_format: str = "real", shard=(0, 1)):
-        """Render one frame (or one shard's strip) into a host array (H, W, 3); returns (image, stats)."""
+               out_format: str = "real", shard=(0, 1), out: np.ndarray | None = None):
+        """Render one frame (or one shard's strip) into a host array (H, W, 3); returns (image, stats).
+        `out` reuses a caller's array of that shape and dtype (a canvas kept across frames)."""
         opts = self.options(depth, precision, out_format, shard)
         rows = camera.height if shard[1] == 1 else shard_rows(camera.height, shard[1])
         dtype = np.uint8 if out_format == "u8" else (np.float32 if precision == "f32" else np.float64)
-        img = np.zeros((rows, camera.width, 3), dtype=dtype)
+        if out is not None:
+            if out.shape != (rows, camera.width, 3) or out.dtype != dtype or not out.flags.c_contiguous:
+                raise ValueError(f"out must be a C-contiguous {dtype.__name__} array of shape {(rows, camera.width, 3)}")
+            img = out
+        else:
+            img = np.zeros((rows, camera.width, 3), dtype=dtype)
         st = Stats()
         _check(_lib.rt_render(self._h, C.byref(camera), C.byref(opts), img.ctypes.data_as(C.c_void_p),
                               C.byref(st)))
