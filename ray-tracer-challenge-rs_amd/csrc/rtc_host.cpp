@@ -13,6 +13,7 @@
 #include <array>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <memory>
 #include <string>
 #include <vector>
@@ -168,7 +169,11 @@ int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes,
             double bs[4];
             bounding_sphere(d, bs);
             for (int q = 0; q < 3; ++q) r.bound[q] = (R)bs[q];
-            r.bound[3] = ctx->cull && bs[3] >= 0.0 ? (R)(bs[3] * bs[3]) : (R)-1;  // device keeps r^2
+            // the device keeps r^2; unbounded is +inf for spheres and cubes
+            // (their test has no branch), -1 for the other kinds (wave_may_hit)
+            const bool branchless = d.kind == RT_SHAPE_SPHERE || d.kind == RT_SHAPE_CUBE;
+            r.bound[3] = ctx->cull && bs[3] >= 0.0 ? (R)(bs[3] * bs[3])
+                                                   : (branchless ? std::numeric_limits<R>::infinity() : (R)-1);
             r.ymin = (R)d.minimum;
             r.ymax = (R)d.maximum;
             for (int q = 0; q < 3; ++q) {

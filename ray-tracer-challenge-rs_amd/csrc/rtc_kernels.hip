@@ -393,10 +393,18 @@ __device__ inline void for_all_kinds(const DevScene<R>& sc, F&& f) {
 // __ballot(int) turns the predicate into a VGPR and compares it again.
 __device__ inline bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 
-template <typename R>
+// Per kind: planes are never bounded (no test, no record load); spheres and
+// cubes always carry a radius, +inf when unbounded (RTC_CULL=0 or a
+// non-finite transform: every finite ray then passes), so their test has no
+// branch on the record and its loads issue together; cylinders, cones and
+// triangles keep a wave-uniform branch on r^2 < 0 (open cylinders and cones
+// are unbounded, their test would be wasted VALU).
+template <typename R, int K>
 __device__ inline bool wave_may_hit(const ShapeRec<R>& s, V3<R> o, V3<R> d) {
+    if constexpr (K == RT_SHAPE_PLANE) return true;
     const R r2 = s.bound[3];  // radius^2
-    if (!(r2 >= (R)0)) return true;  // unbounded shape: wave-uniform
+    if constexpr (K != RT_SHAPE_SPHERE && K != RT_SHAPE_CUBE)
+        if (!(r2 >= (R)0)) return true;  // unbounded shape: wave-uniform
     const V3<R> oc = {s.bound[0] - o.x, s.bound[1] - o.y, s.bound[2] - o.z};
     // |d x oc|^2 = |oc|^2 |d|^2 - (oc.d)^2 (Lagrange): reuses oc.d of the
     // front test.  Rounding of the two products is bounded by ~12 ulp of
@@ -471,7 +479,7 @@ template <typename R>
 __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
     Nearest<R> best;
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
-        if (!wave_may_hit(s, o, d)) return;
+        if (!wave_may_hit<R, K>(s, o, d)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
         const int w = s.world_index;
@@ -510,7 +518,7 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) 
     Blocker<R> b;
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
         if (!s.casts_shadow) return;  // wave-uniform
-        if (!wave_may_hit(s, o, d)) return;
+        if (!wave_may_hit<R, K>(s, o, d)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
         entries<R, K>(s, lo, ld, [&](R t, bool v) { b.offer(t, v, dist); });
