@@ -293,6 +293,17 @@ int rt_debug_intersect(rt_context* ctx, uint32_t shape, const double* rays, uint
 int rt_debug_normal(rt_context* ctx, uint32_t shape, const double* points, uint64_t n_points, uint32_t precision,
                     uint32_t world_space, double* out);
 
+/* Per-scene kernels.  For f32 frames the library compiles (hipRTC), once
+ * per uploaded world, the same tracer source with the world's shape table as
+ * compile-time constants, and runs it instead of the generic kernel (same
+ * pixels, bit for bit).  mode 0 = never, 1 = every f32 frame, 2 = frames of
+ * at least 64K pixels (the default; env RTC_JIT=0|1 overrides at context
+ * creation).  rt_jit_status: whether the last launch ran a per-scene kernel,
+ * the compile milliseconds spent by this context, and the last build error
+ * (a failed build keeps the generic kernel for that world). */
+int rt_context_set_jit(rt_context* ctx, int mode);
+int rt_jit_status(rt_context* ctx, int* used_last_launch, double* compile_ms, char* log, size_t log_len);
+
 /* Cumulative device counters since context creation (after a sync). */
 int rt_read_counters(rt_context* ctx, rt_stats* totals);
 

@@ -95,6 +95,17 @@ struct rt_context {
     uint32_t stamp_capacity = 0, stamp_count = 0;
     void* d_scratch = nullptr;  // host-buffer renders / color_at staging
     size_t scratch_bytes = 0;
+    // Per-scene f32 kernels (rtc_jit.cpp): the f32 shape table of the last
+    // upload, the kernels built for it (direct/pool x global/LDS world), and
+    // RTC_JIT = 0 (never) | 1 (every f32 frame) | auto (frames of at least
+    // kJitMinTiles tiles; small frames are not worth a build)
+    std::vector<rtc::ShapeRec<float>> jit_shapes;
+    int32_t jit_begin[rtc::kNumKinds + 1] = {};
+    hipFunction_t jit_fn[4] = {};
+    int jit_mode = 2;
+    bool jit_failed = false, jit_used = false;
+    double jit_compile_ms = 0;
+    std::string jit_log;
     // rt_render: counters before/after and the error flag come back pinned,
     // on the stream, so a frame needs one host sync
     unsigned long long* h_counters = nullptr;  // 2 x kCounterShards x kNumCounters + the error flag
@@ -134,8 +145,14 @@ int validate_scene(const rt_shape_desc* shapes, uint32_t ns, const rt_material_d
 int build_scene(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats, uint32_t nm,
                 const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights, uint32_t nl);
 // One frame (or shard strip) of this device into `out_device` on `stream`.
+int capture_jit_table(rt_context* ctx);  // the f32 table of the uploaded world, for rtc_jit.cpp
 int launch_frame(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, uint32_t shard_index,
                  uint32_t shard_count, void* out_device, hipStream_t stream);
+// rtc_jit.cpp: the per-scene kernel of this context's world for a launch of
+// `static_blocks` workgroups per CU, or null (use the generic kernel)
+constexpr uint32_t kJitMinTiles = 256;  // 64K pixels
+int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int static_blocks, hipFunction_t* fn);
+
 // rtc_group.cpp: the same entry points on a multi-GPU context
 int group_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats,
                        uint32_t nm, const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights,

@@ -293,6 +293,7 @@ constexpr size_t kStaticLds = 256;
 constexpr size_t kMaxLds = kLdsPerCu - 8 * 1024;  // dynamic LDS of one workgroup (room for static)
 
 struct LaunchShape {
+    int per_cu;  // workgroups per CU the launch is planned for
     bool pool;
     uint32_t world_lds;  // world tables staged in LDS (bytes, 0 = none)
     uint32_t sched;
@@ -383,6 +384,7 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
     int per_cu = 0;
     if ((rc = blocks_per_cu<R>(ctx, ls.pool, ls.world_lds != 0, ls.lds, &per_cu))) return rc;
     if (per_cu < 1) per_cu = 1;
+    ls.per_cu = per_cu;
     const uint64_t resident = (uint64_t)per_cu * (uint64_t)ctx->cu_count;
     // The f32 direct kernel's static schedule runs 2.5x the resident grid: the
     // dispatcher starts the surplus workgroups as resident ones finish, which
@@ -536,6 +538,28 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     // kernel whose containers walk aggregates per class
     const bool dup = ctx->duplicate_shapes > 0;
     const bool sp = sizeof(R) == 4 && ls.pool && ctx->kind_variants && (kinds & ~kKindsSp) == 0 && !dup;
+    // large f32 frames run the per-scene build of the same kernel (rtc_jit.cpp)
+    hipFunction_t jf = nullptr;
+    if constexpr (sizeof(R) == 4) {
+        const bool want = cam && !dup && !(flags & RT_FLAG_STAMPS) &&
+                          (ctx->jit_mode == 1 || (ctx->jit_mode == 2 && P.n_tiles >= kJitMinTiles));
+        if (want && (rc = jit_function(ctx, ls.pool, ls.world_lds != 0, ls.lds, ls.per_cu, &jf))) return rc;
+    }
+    ctx->jit_used = jf != nullptr;
+    if (jf) {
+        if (!ls.pool) {  // the per-scene direct kernel takes one tile per workgroup
+            P.persistent = kSchedGrid;
+            ls.grid = P.n_tiles;
+        }
+        const ShapeRec<R>* sh = P.scene.shapes;
+        const MaterialRec<R>* mt = P.scene.materials;
+        const PatternRec<R>* pt = P.scene.patterns;
+        const LightRec<R>* lt = P.scene.lights;
+        void* args[] = {&P, &sh, &mt, &pt, &lt};
+        (void)hipGetLastError();
+        RT_HIP(hipModuleLaunchKernel(jf, ls.grid, 1, 1, kBlock, 1, 1, (unsigned)ls.lds, stream, args, nullptr));
+        return RT_OK;
+    }
     if (hipError_t e = sp ? sp::launch_trace<R>(P, ls.pool, dup, ls.grid, ls.lds, stream)
                           : launch_trace<R>(P, ls.pool, dup, ls.grid, ls.lds, stream);
         e != hipSuccess)
@@ -694,6 +718,7 @@ int create_device_context(int device_ordinal, rt_context** out) {
     if (const char* e = std::getenv("RTC_POOL_LDS_RAYS")) ctx->pool_lds_rays = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("RTC_TILE_ORDER")) ctx->tile_order = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_DIRECT_GRID")) ctx->direct_grid = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("RTC_JIT")) ctx->jit_mode = !std::strcmp(e, "0") ? 0 : !std::strcmp(e, "1") ? 1 : 2;
     RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreate(&ctx->ev_start));
     RT_HIP(hipEventCreate(&ctx->ev_stop));
@@ -764,6 +789,7 @@ int build_scene(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const
     std::vector<uint32_t> cls;  // value-identity classes (shape_identity.hpp)
     ctx->duplicate_shapes = ident::shape_classes(shapes, ns, mats, pats, cls);
     if ((rc = build_world<float>(ctx, ctx->w32, shapes, ns, mats, nm, pats, np, lights, nl, cls))) return rc;
+    if ((rc = capture_jit_table(ctx))) return rc;
     if ((rc = build_world<double>(ctx, ctx->w64, shapes, ns, mats, nm, pats, np, lights, nl, cls))) return rc;
     ctx->flops = FlopScene{};
     for (uint32_t i = 0; i < ns; ++i) {
@@ -773,6 +799,17 @@ int build_scene(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const
     ctx->flops.n_lights = nl;
     ctx->have_scene = true;
     ++ctx->scene_gen;  // invalidates the recorded tile costs
+    return RT_OK;
+}
+
+int capture_jit_table(rt_context* ctx) {
+    const int32_t n = ctx->w32.scene.kind_begin[kNumKinds];
+    ctx->jit_shapes.assign(n, ShapeRec<float>{});
+    if (n) RT_HIP(hipMemcpy(ctx->jit_shapes.data(), ctx->w32.shapes, n * sizeof(ShapeRec<float>), hipMemcpyDeviceToHost));
+    for (int k = 0; k <= kNumKinds; ++k) ctx->jit_begin[k] = ctx->w32.scene.kind_begin[k];
+    for (auto& f : ctx->jit_fn) f = nullptr;
+    ctx->jit_failed = false;
+    ctx->jit_log.clear();
     return RT_OK;
 }
 
@@ -956,6 +993,24 @@ int rt_debug_intersect(rt_context* ctx, uint32_t shape, const double* rays, uint
 int rt_debug_normal(rt_context* ctx, uint32_t shape, const double* points, uint64_t n, uint32_t precision,
                     uint32_t world_space, double* out) {
     return debug_shape(ctx, shape, 1, points, 3, n, precision, world_space, out, 3);
+}
+
+int rt_context_set_jit(rt_context* ctx, int mode) {
+    if (!ctx || mode < 0 || mode > 2) return set_error(RT_ERR_INVALID, "bad arguments");
+    ctx->jit_mode = mode;
+    for (rt_context* p : ctx->peers) p->jit_mode = mode;
+    return RT_OK;
+}
+
+int rt_jit_status(rt_context* ctx, int* used_last_launch, double* compile_ms, char* log, size_t log_len) {
+    if (!ctx) return set_error(RT_ERR_INVALID, "null context");
+    if (used_last_launch) *used_last_launch = ctx->jit_used ? 1 : 0;
+    if (compile_ms) *compile_ms = ctx->jit_compile_ms;
+    if (log && log_len) {
+        std::strncpy(log, ctx->jit_log.c_str(), log_len - 1);
+        log[log_len - 1] = '\0';
+    }
+    return RT_OK;
 }
 
 int rt_debug_stamps(rt_context* ctx, uint64_t* out, uint32_t max_wg, uint32_t* n) {

@@ -14,7 +14,9 @@
 #pragma once
 
 #include <cstdint>
+#ifndef __HIPCC_RTC__
 #include <string>
+#endif
 
 #include "../../include/rtc.h"
 
@@ -26,7 +28,9 @@
 
 namespace rtc {
 
+#ifndef __HIPCC_RTC__
 int set_error(int code, const std::string& msg);  // rtc_host.cpp (thread-local)
+#endif
 
 // Row-block shards: tile row k of the image (RT_TILE_H rows)
 // belongs to shard k % shards, which renders its tile rows in order into a

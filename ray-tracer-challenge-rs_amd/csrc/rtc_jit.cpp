@@ -1,0 +1,205 @@
+// rtc_jit.cpp — per-scene builds of the f32 tracer kernels (hipRTC).
+//
+// The generic kernels walk the world's shape table with wave-uniform scalar
+// loads: every shape of every ray costs a dependent s_load round trip, loop
+// control and per-record branches.  For a large frame the
+// library instead compiles, once per uploaded world, the same kernel source
+// (embedded in librtc, rtc_kernels.hip) with the f32 shape table as a
+// constexpr array and each kind's loop unrolled at compile time
+// (rtc_kernels.hip `jit_each`): every record field becomes a constant of the
+// instruction stream.  The arithmetic is the same source with the same
+// operations on the same values, so frames are bit-identical to the generic
+// kernel (tests/test_gpu_jit.py); only the f32 frame kernels are built this
+// way (the f64 parity path, rt_color_at and small frames keep the generic
+// kernels).  Builds are cached per process by table content and device, and
+// a failed build falls back to the generic kernel for that world.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rtc_context.hpp"
+#include "rtc_jit_sources.inc"  // kSrcKernels, kSrcInternal, kSrcRtcH (tools/embed_sources.py)
+
+namespace rtc {
+namespace {
+
+std::string hexf(float v) {
+    uint32_t b;
+    std::memcpy(&b, &v, 4);
+    char buf[48];
+    std::snprintf(buf, sizeof buf, "__builtin_bit_cast(float, 0x%08xu)", b);
+    return buf;
+}
+
+template <size_t N>
+std::string floats(const float (&a)[N]) {
+    std::string s = "{";
+    for (size_t i = 0; i < N; ++i) s += (i ? ", " : "") + hexf(a[i]);
+    return s + "}";
+}
+
+// rtc_jit_scene.hpp: the world's f32 shape table as constexpr data.
+std::string scene_header(const std::vector<ShapeRec<float>>& sh, const int32_t begin[kNumKinds + 1]) {
+    std::string s = "#pragma once\n#include \"rtc_internal.hpp\"\nnamespace rtc {\nnamespace jit {\n";
+    s += "constexpr int kBegin[" + std::to_string(kNumKinds + 1) + "] = {";
+    for (int k = 0; k <= kNumKinds; ++k) s += (k ? ", " : "") + std::to_string(begin[k]);
+    s += "};\nconstexpr ShapeRec<float> kShapes[" + std::to_string(sh.size() + 1) + "] = {\n";
+    for (const ShapeRec<float>& r : sh) {
+        s += "    {" + floats(r.inv) + ", " + floats(r.bound) + ", " + std::to_string(r.world_index) + ", " +
+             std::to_string(r.casts_shadow) + ", " + std::to_string(r.material) + ", " + std::to_string(r.flags) +
+             ", " + hexf(r.ymin) + ", " + hexf(r.ymax) + ", " + floats(r.tri) + "},\n";
+    }
+    s += "    {}};\n}  // namespace jit\n}  // namespace rtc\n";
+    return s;
+}
+
+uint64_t fnv(const void* p, size_t n, uint64_t h = 1469598103934665603ull) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+}
+
+const char* kernel_name(bool pool, bool lds) {
+    if (pool) return lds ? "rtc::trace_pool<float, true, false>" : "rtc::trace_pool<float, false, false>";
+    return lds ? "rtc::trace_direct<float, true>" : "rtc::trace_direct<float, false>";
+}
+
+struct CodeObject {
+    std::vector<char> code;
+    std::string lowered;
+    double compile_ms = 0;
+};
+
+// Process-wide caches: code objects by (table, kernel); loaded functions by
+// (code object, device).
+std::mutex g_mu;
+std::map<std::pair<uint64_t, int>, std::shared_ptr<CodeObject>> g_code;
+std::map<std::pair<uint64_t, int>, std::pair<hipModule_t, hipFunction_t>> g_fn;
+
+int compile(const std::string& scene, const char* name, CodeObject& out, std::string& log) {
+    const std::string main_src = std::string("#define RTC_JIT 1\n#include \"rtc_jit_scene.hpp\"\n") + kSrcKernels;
+    const char* headers[] = {scene.c_str(), kSrcInternal, kSrcRtcH};
+    const char* names[] = {"rtc_jit_scene.hpp", "rtc_internal.hpp", "../../include/rtc.h"};
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, main_src.c_str(), "rtc_kernels_scene.hip", 3, headers, names) != HIPRTC_SUCCESS)
+        return set_error(RT_ERR_HIP, "hiprtcCreateProgram failed");
+    hiprtcAddNameExpression(prog, name);
+    // the flags of the static build (Makefile): no contraction beyond the
+    // source's explicit fmas, no SLP packing
+    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-fno-slp-vectorize"};
+    const auto t0 = std::chrono::steady_clock::now();
+    const hiprtcResult r = hiprtcCompileProgram(prog, 5, opts);
+    out.compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    log.assign(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &log[0]);
+    int rc = RT_OK;
+    if (r != HIPRTC_SUCCESS) {
+        rc = set_error(RT_ERR_HIP, std::string("hiprtcCompileProgram: ") + hiprtcGetErrorString(r) + "\n" + log);
+    } else {
+        const char* lowered = nullptr;
+        hiprtcGetLoweredName(prog, name, &lowered);
+        out.lowered = lowered ? lowered : "";
+        size_t cs = 0;
+        hiprtcGetCodeSize(prog, &cs);
+        out.code.resize(cs);
+        hiprtcGetCode(prog, out.code.data());
+        if (out.lowered.empty() || cs == 0) rc = set_error(RT_ERR_HIP, "hipRTC produced no kernel");
+        if (const char* dir = std::getenv("RTC_JIT_DUMP")) {  // diagnostics: scene header + code object
+            const std::string base = std::string(dir) + "/" + std::to_string(fnv(scene.data(), scene.size())) + "_" +
+                                     (std::strstr(name, "pool") ? "pool" : "direct");
+            if (FILE* f = std::fopen((base + ".hpp").c_str(), "w")) {
+                std::fwrite(scene.data(), 1, scene.size(), f);
+                std::fclose(f);
+            }
+            if (FILE* f = std::fopen((base + ".co").c_str(), "wb")) {
+                std::fwrite(out.code.data(), 1, out.code.size(), f);
+                std::fclose(f);
+            }
+        }
+    }
+    hiprtcDestroyProgram(&prog);
+    return rc;
+}
+
+}  // namespace
+
+// The per-scene kernel for this context's uploaded world, or null (use the
+// generic kernel): compiled on first use per world and kernel variant.
+int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int static_blocks, hipFunction_t* fn) {
+    *fn = nullptr;
+    if (ctx->jit_failed || ctx->jit_shapes.empty()) return RT_OK;
+    // Only the direct kernel is built per scene.  The pool kernel's
+    // generation loop keeps the unrolled record constants live across
+    // generations: 312-608 B/lane of scratch and 2.3-2.8x the generic
+    // kernel's time (reflect_refract, table).
+    if (pool) return RT_OK;
+    const int variant = (pool ? 2 : 0) + (lds ? 1 : 0);
+    if (ctx->jit_fn[variant]) {
+        *fn = ctx->jit_fn[variant];
+        return RT_OK;
+    }
+    const uint64_t key = fnv(ctx->jit_begin, sizeof ctx->jit_begin,
+                             fnv(ctx->jit_shapes.data(), ctx->jit_shapes.size() * sizeof(ShapeRec<float>)));
+    std::shared_ptr<CodeObject> co;
+    std::string log;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_code.find({key, variant});
+        if (it != g_code.end()) co = it->second;
+    }
+    if (!co) {
+        auto built = std::make_shared<CodeObject>();
+        if (compile(scene_header(ctx->jit_shapes, ctx->jit_begin), kernel_name(pool, lds), *built, log)) {
+            ctx->jit_failed = true;  // keep the generic kernel for this world
+            ctx->jit_log = rt_last_error();
+            return RT_OK;
+        }
+        ctx->jit_compile_ms += built->compile_ms;
+        std::lock_guard<std::mutex> lk(g_mu);
+        co = g_code.emplace(std::make_pair(key, variant), built).first->second;
+    }
+    std::pair<hipModule_t, hipFunction_t> mf{};
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_fn.find({(uint64_t)(uintptr_t)co.get(), ctx->device});
+        if (it != g_fn.end()) mf = it->second;
+    }
+    if (!mf.second) {
+        RT_HIP(hipSetDevice(ctx->device));
+        RT_HIP(hipModuleLoadData(&mf.first, co->code.data()));
+        RT_HIP(hipModuleGetFunction(&mf.second, mf.first, co->lowered.c_str()));
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_fn[{(uint64_t)(uintptr_t)co.get(), ctx->device}] = mf;
+    }
+    // The launch is planned with the generic kernel's occupancy: use the
+    // per-scene kernel only if it keeps at least as many workgroups per CU,
+    // and only if it does not spill.  Unrolled over many shapes, the
+    // compiler keeps record constants live across the body and spills them
+    // (shadow_puppets' 8 spheres: 56 B/lane of scratch, +10 % against the
+    // generic kernel; three_sphere's 6 shapes: none, -17 %).
+    int blocks = 0, scratch = 0;
+    RT_HIP(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mf.second, kBlock, dyn_lds));
+    RT_HIP(hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, mf.second));
+    if (blocks < static_blocks || scratch > 0) {
+        ctx->jit_failed = true;
+        ctx->jit_log = "per-scene kernel not used: " + std::to_string(blocks) + " workgroups/CU (generic " +
+                       std::to_string(static_blocks) + "), " + std::to_string(scratch) + " B/lane of scratch";
+        return RT_OK;
+    }
+    ctx->jit_fn[variant] = mf.second;
+    *fn = mf.second;
+    return RT_OK;
+}
+
+}  // namespace rtc

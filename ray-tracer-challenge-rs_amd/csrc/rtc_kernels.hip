@@ -31,11 +31,11 @@
 // shape loops of those kinds only (rtc::<namespace>::launch_trace).  Same
 // code for the kinds it keeps, so the same pixels; the host uses it for
 // worlds whose kinds it covers (rtc_host.cpp, pool_variant).
+#ifndef __HIPCC_RTC__  // hipRTC (per-scene build, rtc_jit.cpp) pre-includes the HIP runtime
 #include <hip/hip_runtime.h>
 
-#include <cfloat>
-#include <climits>
 #include <cstdint>
+#endif
 
 #include "rtc_internal.hpp"
 
@@ -53,7 +53,7 @@ struct Real<float> {
     static constexpr float kEps = 8e-8f;        // guards (consts.rs:2)
     static constexpr float kOffset = 1e-4f;     // over/under point + cap normals:
                                                 // 8e-8 is below the f32 ulp at |p|>0.7
-    static constexpr float kMax = FLT_MAX;      // consts.rs:8 analogue
+    static constexpr float kMax = __FLT_MAX__;  // consts.rs:8 analogue
     static constexpr float kInf = __builtin_huge_valf();
     // reference `a * b + c` (unfused there): fused here for throughput
     __device__ static inline float madd(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
@@ -76,7 +76,7 @@ template <>
 struct Real<double> {
     static constexpr double kEps = 0.00000008;
     static constexpr double kOffset = 0.00000008;  // computed_hit.rs:33-34
-    static constexpr double kMax = DBL_MAX;
+    static constexpr double kMax = __DBL_MAX__;
     static constexpr double kInf = __builtin_huge_val();
     __device__ static inline double madd(double a, double b, double c) { return a * b + c; }
     __device__ static inline double rfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
@@ -350,9 +350,29 @@ __device__ inline T ld_uniform(const T* p) {
     return *p;
 }
 
+#ifdef RTC_JIT
+// Per-scene build (rtc_jit.cpp): the f32 shape table is a constexpr array
+// (rtc_jit_scene.hpp, generated at upload) and each kind's loop is unrolled
+// at compile time, so every record field is a constant of the instruction
+// stream — no scalar loads, no loop control, no per-record branches.
+template <int I, int E, typename F>
+__device__ inline void jit_each(F&& f) {
+    if constexpr (I < E) {
+        f(jit::kShapes[I], I);
+        jit_each<I + 1, E>(f);
+    }
+}
+#endif
+
 // Visit every shape of kind K (wave-uniform loop, scalar loads).
 template <typename R, int K, typename F>
 __device__ inline void for_kind(const DevScene<R>& sc, F&& f) {
+#ifdef RTC_JIT
+    if constexpr (sizeof(R) == 4) {
+        jit_each<jit::kBegin[K], jit::kBegin[K + 1]>(f);
+        return;
+    }
+#endif
     const int b = sc.kind_begin[K], e = sc.kind_begin[K + 1];
     for (int i = b; i < e; ++i) {
         const ShapeRec<R> s = ld_uniform(&sc.shapes[i]);
@@ -443,7 +463,7 @@ template <typename R>
 struct Nearest {
     static constexpr bool kKeys = sizeof(R) == 4 && RTC_VALU_KEYS;
     R t = Real<R>::kInf;
-    int w = INT_MAX;
+    int w = __INT_MAX__;
     unsigned long long key = 0x7F8000007FFFFFFFull;  // (+inf, INT_MAX)
     __device__ inline void offer(R te, bool v, int we) {
         if constexpr (kKeys) {
@@ -461,7 +481,7 @@ struct Nearest {
     __device__ inline Hit<R> hit(const DevScene<R>& sc) const {
         const int hw = kKeys ? (int)(uint32_t)key : w;
         Hit<R> h{t, -1, hw, -1};
-        if (hw != INT_MAX) {
+        if (hw != __INT_MAX__) {
             const uint32_t ws = (uint32_t)sc.lworld_slot[hw];
             h.slot = (int)(ws & 0xFFFFFFu);
             h.kind = (int)(ws >> 24);
@@ -1106,6 +1126,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         }
         count_events(k, valid, hit, sh, sc.n_lights);
         if (valid) store_pixel(P, out_idx, c);
+#ifdef RTC_JIT
+        // the per-scene build runs one tile per workgroup (rtc_host.cpp): a
+        // straight-line body, so no record constant is hoisted out of the
+        // tile loop and held (spilled) across it
+        break;
+#endif
     }
     if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
     if (P.stamps) {
@@ -1295,6 +1321,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     }
 }
 
+#ifndef RTC_JIT  // the per-scene build (rtc_jit.cpp) holds the tracer kernels only
 // Heaviest-first tile order from the previous launch's per-tile costs: a
 // one-workgroup bucket sort (8 buckets per octave of cost, descending).  The
 // pool kernel's time is set by its last, heaviest tiles (a glass-sphere tile
@@ -1495,6 +1522,7 @@ hipError_t launch_assemble(const void* gathered, void* image, uint32_t width, ui
 }
 
 #endif  // !RTC_VARIANT
+#endif  // !RTC_JIT
 #ifdef RTC_VARIANT
 }  // namespace RTC_VARIANT
 #endif

@@ -177,6 +177,8 @@ def _load() -> C.CDLL:
         "rt_comm_unique_id": (C.c_int, [P(C.c_uint8)]),
         "rt_context_create_rank": (C.c_int, [C.c_int, C.c_int, C.c_int, P(C.c_uint8), P(C.c_void_p)]),
         "rt_context_group": (C.c_int, [C.c_void_p, P(C.c_int), P(C.c_int), P(C.c_int)]),
+        "rt_context_set_jit": (C.c_int, [C.c_void_p, C.c_int]),
+        "rt_jit_status": (C.c_int, [C.c_void_p, P(C.c_int), P(C.c_double), C.c_char_p, C.c_size_t]),
         "rt_debug_intersect": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), C.c_uint64, C.c_uint32, C.c_uint32,
                                          P(C.c_double)]),
         "rt_debug_normal": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), C.c_uint64, C.c_uint32, C.c_uint32,
@@ -199,6 +201,7 @@ EXPORTED_SYMBOLS = (
     "rt_scene_upload", "rt_shard_rows", "rt_render", "rt_render_device", "rt_color_at", "rt_read_counters",
     "rt_debug_stamps", "rt_debug_tile_costs", "rt_debug_intersect", "rt_debug_normal", "rt_camera_set_transform",
     "rt_shard_row_map", "rt_context_create_multi", "rt_comm_unique_id", "rt_context_create_rank", "rt_context_group",
+    "rt_context_set_jit", "rt_jit_status",
     "rt_assemble_shards", "rt_scene_load_yaml", "rt_scene_load_yaml_text", "rt_scene_view_get", "rt_scene_free",
     "rt_camera_make", "rt_camera_resize", "rt_matrix_inverse",
 )
@@ -378,6 +381,16 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def set_jit(self, mode: int) -> None:
+        """Per-scene kernels: 0 never, 1 every f32 frame, 2 frames of >= 64K pixels (rtc.h rt_context_set_jit)."""
+        _check(_lib.rt_context_set_jit(self._h, mode))
+
+    def jit_status(self) -> dict:
+        """Whether the last launch ran a per-scene kernel, compile ms so far, last build error."""
+        used, ms, log = C.c_int(), C.c_double(), C.create_string_buffer(4096)
+        _check(_lib.rt_jit_status(self._h, C.byref(used), C.byref(ms), log, len(log)))
+        return {"used": bool(used.value), "compile_ms": ms.value, "log": log.value.decode(errors="replace")}
 
     def upload(self, scene: SceneTables | None) -> None:
         """rt_scene_upload; on a non-zero rank of a group, None (the scene comes from rank 0)."""

@@ -1,0 +1,84 @@
+"""Per-scene kernels (csrc/rtc_jit.cpp) against the generic kernels.
+
+For f32 frames the library compiles the tracer source once per uploaded
+world with the shape table as compile-time constants (hipRTC).  Same source,
+same operations, same values: every frame must equal the generic kernel's
+bit for bit, counters included, for every reference scene and for a world
+with every shape and pattern kind.  (Parity with the oracle then carries
+over from tests/test_gpu_parity.py, which runs the generic kernels; the
+full-size tests in tests/test_gpu_fullsize.py run the per-scene kernels,
+their frames being above the 64K-pixel default threshold.)
+"""
+import numpy as np
+import pytest
+
+from conftest import scene_fixture
+
+pytestmark = pytest.mark.gpu
+
+SCENES = ["three_sphere_scene", "reflect_refract", "cover", "table", "cylinders", "metal", "refraction",
+          "shadow_puppets"]
+
+
+def _counts(st):
+    return {k: st[k] for k in ("primary", "shadow", "reflect", "refract", "shaded", "lit_patterned",
+                               "refract_evals", "schlick_evals")}
+
+
+def _both(gpu_ctx, tables, cam, depth=6):
+    """(generic frame, stats, per-scene frame, stats, repeat) — the per-scene
+    frame is None when the library declined to use its build (pool-kernel
+    worlds, or a build that spills; jit_status() says why)."""
+    gpu_ctx.upload(tables)
+    gpu_ctx.set_jit(0)
+    a, sa = gpu_ctx.render(cam, depth, precision="f32")
+    assert not gpu_ctx.jit_status()["used"]
+    gpu_ctx.set_jit(1)
+    try:
+        b, sb = gpu_ctx.render(cam, depth, precision="f32")
+        st = gpu_ctx.jit_status()
+        if not st["used"]:
+            assert depth > 0 and tables.has_secondary() or "not used" in st["log"], st["log"][:2000]
+            return a, sa, None, None, None
+        b2, _ = gpu_ctx.render(cam, depth, precision="f32")
+    finally:
+        gpu_ctx.set_jit(2)
+    return a, sa, b, sb, b2
+
+
+
+
+
+@pytest.mark.parametrize("name", SCENES)
+@pytest.mark.parametrize("depth", [0, 6])
+def test_per_scene_kernel_is_bit_identical(gpu_ctx, rtc, name, depth):
+    """Depth 0 runs the direct kernel on every scene (no child rays)."""
+    scene = scene_fixture(name)
+    cam = rtc.camera_resize(scene.camera, 320, 200)
+    a, sa, b, sb, b2 = _both(gpu_ctx, scene, cam, depth)
+    if name == "three_sphere_scene":
+        assert b is not None, "the headline scene must run its per-scene kernel"
+    if b is None:
+        return
+    assert np.array_equal(a, b) and np.array_equal(a, b2), f"{name}: {int((a != b).any(axis=2).sum())} px differ"
+    assert _counts(sa) == _counts(sb)
+
+
+def test_per_scene_kernel_all_kinds(gpu_ctx):
+    from test_gpu_parity import _all_shapes_world
+    from rtc_amd import world as W
+    cam = W.camera(160, 120, 1.0, (0, 3, -8), (0, 0.8, 0), (0, 1, 0))
+    a, sa, b, sb, _ = _both(gpu_ctx, _all_shapes_world(), cam, 0)
+    if b is not None:
+        assert np.array_equal(a, b) and _counts(sa) == _counts(sb)
+
+
+def test_default_threshold_uses_the_per_scene_kernel_for_large_frames(gpu_ctx, rtc):
+    scene = scene_fixture("three_sphere_scene")
+    gpu_ctx.upload(scene)
+    gpu_ctx.render(rtc.camera_resize(scene.camera, 64, 64), 6, precision="f32")
+    assert not gpu_ctx.jit_status()["used"]
+    gpu_ctx.render(rtc.camera_resize(scene.camera, 640, 480), 6, precision="f32")
+    assert gpu_ctx.jit_status()["used"]
+    gpu_ctx.render(rtc.camera_resize(scene.camera, 640, 480), 6, precision="f64")
+    assert not gpu_ctx.jit_status()["used"]  # the f64 parity path is never rebuilt
