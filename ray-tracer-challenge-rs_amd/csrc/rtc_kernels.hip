@@ -439,6 +439,18 @@ __device__ inline bool wave_may_hit(const ShapeRec<R>& s, V3<R> o, V3<R> d) {
     return (front & __builtin_amdgcn_ballot_w64(Real<R>::madd(oo, kKeep, -r2) * dot(d, d) <= tc * tc)) != 0;
 }
 
+// Per-scene build only: the ray's registers pass through an empty asm at the
+// top of each unrolled shape, so the compiler cannot hoist every shape's
+// ray-dependent terms (the cull's |o - c|^2, ...) to the front of the
+// unrolled sequence, where they stay live and spill.  A no-op otherwise.
+template <typename R>
+__device__ inline void jit_fence(V3<R>& o, V3<R>& d) {
+#if defined(RTC_JIT) && !defined(RTC_JIT_NO_FENCE)
+    if constexpr (sizeof(R) == 4)
+        asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z), "+v"(d.x), "+v"(d.y), "+v"(d.z));
+#endif
+}
+
 template <typename R>
 struct Hit {
     R t;
@@ -499,6 +511,7 @@ template <typename R>
 __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
     Nearest<R> best;
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
+        jit_fence(o, d);
         if (!wave_may_hit<R, K>(s, o, d)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
@@ -538,6 +551,7 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) 
     Blocker<R> b;
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
         if (!s.casts_shadow) return;  // wave-uniform
+        jit_fence(o, d);
         if (!wave_may_hit<R, K>(s, o, d)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
@@ -595,6 +609,7 @@ __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> 
     };
     // entries of one shape before the hit: their count and the latest
     auto scan = [&]<int K>(const ShapeRec<R>& s, int& count, Key& last) {
+        jit_fence(o, d);
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
         const int w = s.world_index;
