@@ -5,7 +5,7 @@ HBM bytes per launch keyed by bench workload, computed as the guide prescribes
 (MI355X_MICROARCH.md "HBM": FETCH_SIZE/WRITE_SIZE are KiB; gfx950 FETCH_SIZE
 counts half of a wide streamed read, so it is doubled).
 
-Usage: python scripts/collect_profiles.py r01
+Usage: python scripts/collect_profiles.py r02
 """
 import collections
 import csv
@@ -17,7 +17,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCENES = {"three_sphere": "three_sphere_scene@1920x1080,depth=5,f32",
-          "reflect_refract": "reflect_refract@1920x1080,depth=6,f32"}
+          "reflect_refract": "reflect_refract@1920x1080,depth=6,f32",
+          "cover": "cover@3840x2160,depth=6,f32",
+          "table": "table@3840x2160,depth=6,f32"}
 
 
 def pmc_means(d, pat="trace_"):
