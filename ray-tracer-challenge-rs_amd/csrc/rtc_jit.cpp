@@ -93,11 +93,16 @@ int compile(const std::string& scene, const char* name, CodeObject& out, std::st
     if (hiprtcCreateProgram(&prog, main_src.c_str(), "rtc_kernels_scene.hip", 3, headers, names) != HIPRTC_SUCCESS)
         return set_error(RT_ERR_HIP, "hiprtcCreateProgram failed");
     hiprtcAddNameExpression(prog, name);
-    // the flags of the static build (Makefile): no contraction beyond the
-    // source's explicit fmas, no SLP packing
-    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-fno-slp-vectorize"};
+    // The flags of the static build (Makefile): no contraction beyond the
+    // source's explicit fmas, no SLP packing.  Plus no machine-level LICM:
+    // with the records as constants it hoists their materialisations (and
+    // values computed from them) out of the generation and tile loops, where
+    // they are held across the loop and spill (reflect_refract's pool kernel:
+    // 100 B/lane of scratch and 106 SGPRs with it, 8 B and 73 VGPRs without).
+    const char* opts[] = {"--offload-arch=gfx950", "-O3",    "-std=c++20", "-ffp-contract=off", "-fno-slp-vectorize",
+                          "-mllvm",                "-disable-machine-licm"};
     const auto t0 = std::chrono::steady_clock::now();
-    const hiprtcResult r = hiprtcCompileProgram(prog, 5, opts);
+    const hiprtcResult r = hiprtcCompileProgram(prog, 7, opts);
     out.compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     size_t n = 0;
     hiprtcGetProgramLogSize(prog, &n);
@@ -139,11 +144,7 @@ int compile(const std::string& scene, const char* name, CodeObject& out, std::st
 int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int static_blocks, hipFunction_t* fn) {
     *fn = nullptr;
     if (ctx->jit_failed || ctx->jit_shapes.empty()) return RT_OK;
-    // Only the direct kernel is built per scene.  The pool kernel's
-    // generation loop keeps the unrolled record constants live across
-    // generations: 312-608 B/lane of scratch and 2.3-2.8x the generic
-    // kernel's time (reflect_refract, table).
-    if (pool) return RT_OK;
+
     const int variant = (pool ? 2 : 0) + (lds ? 1 : 0);
     if (ctx->jit_fn[variant]) {
         *fn = ctx->jit_fn[variant];
@@ -184,14 +185,13 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
     }
     // The launch is planned with the generic kernel's occupancy: use the
     // per-scene kernel only if it keeps at least as many workgroups per CU,
-    // and only if it does not spill.  Unrolled over many shapes, the
-    // compiler keeps record constants live across the body and spills them
-    // (shadow_puppets' 8 spheres: 56 B/lane of scratch, +10 % against the
-    // generic kernel; three_sphere's 6 shapes: none, -17 %).
+    // and only if it spills no more than the generic kernel (direct: none;
+    // pool: 8 B/lane).  A spilling build ran slower than the generic kernel
+    // (shadow_puppets before the ray fence: 56 B/lane, +10 %).
     int blocks = 0, scratch = 0;
     RT_HIP(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mf.second, kBlock, dyn_lds));
     RT_HIP(hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, mf.second));
-    if (blocks < static_blocks || scratch > 0) {
+    if (blocks < static_blocks || scratch > (pool ? 8 : 0)) {
         ctx->jit_failed = true;
         ctx->jit_log = "per-scene kernel not used: " + std::to_string(blocks) + " workgroups/CU (generic " +
                        std::to_string(static_blocks) + "), " + std::to_string(scratch) + " B/lane of scratch";
