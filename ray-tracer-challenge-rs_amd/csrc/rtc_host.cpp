@@ -547,10 +547,6 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     }
     ctx->jit_used = jf != nullptr;
     if (jf) {
-        if (!ls.pool) {  // the per-scene direct kernel takes one tile per workgroup
-            P.persistent = kSchedGrid;
-            ls.grid = P.n_tiles;
-        }
         const ShapeRec<R>* sh = P.scene.shapes;
         const MaterialRec<R>* mt = P.scene.materials;
         const PatternRec<R>* pt = P.scene.patterns;

@@ -1141,12 +1141,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         }
         count_events(k, valid, hit, sh, sc.n_lights);
         if (valid) store_pixel(P, out_idx, c);
-#ifdef RTC_JIT
-        // the per-scene build runs one tile per workgroup (rtc_host.cpp): a
-        // straight-line body, so no record constant is hoisted out of the
-        // tile loop and held (spilled) across it
-        break;
-#endif
     }
     if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
     if (P.stamps) {
