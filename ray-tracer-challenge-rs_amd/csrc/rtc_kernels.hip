@@ -587,23 +587,27 @@ __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> 
     // The hit's own entry is the first of its shape at t == h.t, so entries
     // of that shape sort before it iff t < h.t: push order 0 says exactly that.
     const Key hk{h.t, h.world, 0};
-    bool have_all = false, have_other = false, hit_present = false;
+    // The three flags share one word: as separate bools, the compiler merged
+    // the branches' stores into one store through a selected pointer, which
+    // put the flags in scratch (a scratch store and load per shape).
+    constexpr int kHaveAll = 1, kHaveOther = 2, kHitPresent = 4;
+    int flags = 0;
     Key best_all{}, best_other{};
     int mat_all = -1, mat_other = -1;
     // a class whose entries before the hit are odd in number is in the list
     auto settle = [&](int count, const Key& last, const ShapeRec<R>& s, bool is_hit_class) {
         if (count & 1) {
-            if (!have_all || before(best_all, last)) {
+            if (!(flags & kHaveAll) || before(best_all, last)) {
                 best_all = last;
                 mat_all = s.material;
-                have_all = true;
+                flags |= kHaveAll;
             }
             if (is_hit_class) {
-                hit_present = true;
-            } else if (!have_other || before(best_other, last)) {
+                flags |= kHitPresent;
+            } else if (!(flags & kHaveOther) || before(best_other, last)) {
                 best_other = last;
                 mat_other = s.material;
-                have_other = true;
+                flags |= kHaveOther;
             }
         }
     };
@@ -641,9 +645,9 @@ __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> 
             settle(count, last, s, slot == h.slot);
         });
     }
-    n1 = have_all ? sc.lmats[mat_all].refractive_index : (R)1;
-    if (hit_present)  // the hit's class leaves the list
-        n2 = have_other ? sc.lmats[mat_other].refractive_index : (R)1;
+    n1 = (flags & kHaveAll) ? sc.lmats[mat_all].refractive_index : (R)1;
+    if (flags & kHitPresent)  // the hit's class leaves the list
+        n2 = (flags & kHaveOther) ? sc.lmats[mat_other].refractive_index : (R)1;
     else              // the hit pushes itself
         n2 = sc.lmats[sc.lshapes[h.slot].material].refractive_index;
 }
