@@ -99,10 +99,23 @@ int compile(const std::string& scene, const char* name, CodeObject& out, std::st
     // values computed from them) out of the generation and tile loops, where
     // they are held across the loop and spill (reflect_refract's pool kernel:
     // 100 B/lane of scratch and 106 SGPRs with it, 8 B and 73 VGPRs without).
-    const char* opts[] = {"--offload-arch=gfx950", "-O3",    "-std=c++20", "-ffp-contract=off", "-fno-slp-vectorize",
-                          "-mllvm",                "-disable-machine-licm"};
+    // A build that overrides the kernels' tuning macros (Makefile EXTRA)
+    // passes them on, so both builds plan the same occupancy.
+    std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3",    "-std=c++20", "-ffp-contract=off",
+                                     "-fno-slp-vectorize",    "-mllvm", "-disable-machine-licm"};
+#define RTC_STR2(x) #x
+#define RTC_STR(x) RTC_STR2(x)
+#ifdef RTC_POOL_WAVES
+    opts.push_back("-DRTC_POOL_WAVES=" RTC_STR(RTC_POOL_WAVES));
+#endif
+#ifdef RTC_DIRECT_WAVES
+    opts.push_back("-DRTC_DIRECT_WAVES=" RTC_STR(RTC_DIRECT_WAVES));
+#endif
+#ifdef RTC_WAVE_W
+    opts.push_back("-DRTC_WAVE_W=" RTC_STR(RTC_WAVE_W));
+#endif
     const auto t0 = std::chrono::steady_clock::now();
-    const hiprtcResult r = hiprtcCompileProgram(prog, 7, opts);
+    const hiprtcResult r = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     out.compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     size_t n = 0;
     hiprtcGetProgramLogSize(prog, &n);
@@ -185,13 +198,13 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
     }
     // The launch is planned with the generic kernel's occupancy: use the
     // per-scene kernel only if it keeps at least as many workgroups per CU,
-    // and only if it spills no more than the generic kernel (direct: none;
-    // pool: 8 B/lane).  A spilling build ran slower than the generic kernel
-    // (shadow_puppets before the ray fence: 56 B/lane, +10 %).
+    // and only if it does not spill (neither generic kernel does).  A
+    // spilling build ran slower than the generic kernel (shadow_puppets
+    // before the ray fence: 56 B/lane, +10 %).
     int blocks = 0, scratch = 0;
     RT_HIP(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mf.second, kBlock, dyn_lds));
     RT_HIP(hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, mf.second));
-    if (blocks < static_blocks || scratch > (pool ? 8 : 0)) {
+    if (blocks < static_blocks || scratch > 0) {
         ctx->jit_failed = true;
         ctx->jit_log = "per-scene kernel not used: " + std::to_string(blocks) + " workgroups/CU (generic " +
                        std::to_string(static_blocks) + "), " + std::to_string(scratch) + " B/lane of scratch";

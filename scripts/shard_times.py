@@ -1,0 +1,38 @@
+"""Predicted multi-GPU render time per rank from one GPU: the kernel time of
+each row-block shard of a frame (what rank s renders at N = shards), warm
+(cost-ordered) launches, median of 5.  Diagnostic for DESIGN.md §6."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ray-tracer-challenge-rs_amd"))
+import rtc_amd  # noqa: E402
+from rtc_amd import scene_io  # noqa: E402
+
+name, w, h = (sys.argv[1], int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else ("cover", 3840, 2160)
+scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{name}.json"))
+cam = rtc_amd.camera_resize(scene.camera, w, h)
+s = torch.cuda.current_stream()
+with rtc_amd.Context(0) as ctx:
+    ctx.upload(scene)
+    for shards in (1, 2, 4, 8):
+        rows = rtc_amd.shard_rows(h, shards)
+        out = torch.empty((rows, w, 3), dtype=torch.uint8, device="cuda")
+        times = []
+        for k in range(shards):
+            for _ in range(3):
+                ctx.render_device(cam, out.data_ptr(), s.cuda_stream, 6, "f32", "u8", (k, shards))
+            ts = []
+            for _ in range(5):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                ctx.render_device(cam, out.data_ptr(), s.cuda_stream, 6, "f32", "u8", (k, shards))
+                e1.record(s)
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            times.append(float(np.median(ts)))
+        print(f"{name} {w}x{h} shards={shards}: per-shard ms " + " ".join(f"{t:.3f}" for t in times)
+              + f"  max {max(times):.3f}  ideal {times[0] * 0 + sum(times) / shards:.3f}", flush=True)
