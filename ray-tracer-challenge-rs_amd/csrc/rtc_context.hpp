@@ -58,7 +58,8 @@ struct rt_context {
     hipEvent_t ev_order = nullptr;
     hipStream_t last_stream = nullptr;
     bool launched = false;
-    unsigned long long* d_tile_counter = nullptr;
+    unsigned long long* d_tile_counter = nullptr;  // two sets of queue heads (launch: dynamic schedule)
+    int head_set = 0;                              // the set the next dynamic launch uses
     unsigned long long* d_counters = nullptr;  // kNumCounters cumulative
     int32_t* d_error = nullptr;
     bool have_scene = false;
@@ -87,6 +88,11 @@ struct rt_context {
     uint32_t order_capacity = 0;
     uint64_t order_sig = 0;
     bool order_valid = false;
+    // Tiles costing more than split_factor x the mean workgroup load are
+    // handed out in parts (order_tiles); RTC_SPLIT=0 never splits.
+    double split_factor = 1.5;
+    int order_builds = 0;        // order_tiles runs for the current signature so far
+    int order_max_builds = 8;    // RTC_ORDER_BUILDS: runs per signature before the order is frozen
     uint64_t scene_gen = 0;      // bumped by every rt_scene_upload
     uint32_t duplicate_shapes = 0;  // shapes value-equal to an earlier one (one identity class)
     std::vector<int32_t> world_slot;  // world index -> slot | kind << 24 of the uploaded table

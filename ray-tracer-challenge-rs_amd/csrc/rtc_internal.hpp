@@ -70,6 +70,12 @@ constexpr int kTileQueues = 8;
 // cache line, so every XCD's dequeues serialized on it (~17 us per 1792
 // dequeues on MI355X).
 constexpr int kQueueStride = 32;
+// Work items of a cost-ordered pool launch: a tile, or one part of a tile
+// split 2 or 4 ways (order_tiles).  item = tile | part << 24 | log2(parts) << 28;
+// part p of a tile split 2^l ways seeds the pixels of waves w with
+// w >> (2 - l) == p.
+constexpr uint32_t kItemTileMask = 0xFFFFFFu;
+constexpr uint32_t kItemPartShift = 24, kItemSplitShift = 28;
 // Tile scheduling modes (RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic)
 constexpr uint32_t kSchedGrid = 0;     // one workgroup per tile; the dispatcher balances
 constexpr uint32_t kSchedDynamic = 1;  // resident grid, per-XCD atomic tile queues
@@ -196,8 +202,10 @@ struct LaunchParams {
     uint32_t world_lds;      // bytes of world tables staged at the start of dynamic LDS (0 = none)
     void* spill;                 // pool overflow: grid x 8 x (pool_capacity - pool_lds_capacity) words
     unsigned long long* stamps;  // RT_FLAG_STAMPS: 2 x grid s_memrealtime values
-    unsigned long long* tile_counter;  // kTileQueues queue heads, kQueueStride apart, zeroed per launch
-    const uint32_t* tile_order;        // queue position -> tile (heaviest first), null = raster order
+    unsigned long long* tile_counter;  // kTileQueues queue heads, kQueueStride apart (zero at launch)
+    unsigned long long* next_tile_counter;  // the heads of the next dynamic launch, zeroed by this one
+    const uint32_t* tile_order;        // queue position -> work item (heaviest first), null = raster order
+    const uint32_t* item_count;        // items in tile_order (>= n_tiles: split tiles), null = n_tiles
     uint32_t* tile_cost;               // pool kernel: per-tile duration (10 ns ticks), null = not recorded
     unsigned long long* counters;      // kCounterShards x kNumCounters cumulative u64
     int32_t* error_flag;               // set nonzero on pool overflow

@@ -995,19 +995,18 @@ __device__ inline void flush_counts(const Counts& k, unsigned long long* global)
             if (k.c[i]) atomicAdd(&global[shard * kNumCounters + i], (unsigned long long)k.c[i]);
 }
 
-// Next tile of this workgroup (called by thread 0 only; `probe` lives in
+// Next work item of this workgroup (called by thread 0 only; `probe` lives in
 // its registers).  kSchedGrid: one workgroup per tile; kSchedStatic: tiles
 // b, b+G, b+2G, ... of a resident grid, no atomics; kSchedDynamic: per-XCD
 // queues, queue q holding tiles q, q+8, ....  A workgroup drains queue
 // b % 8 (its XCD's under round-robin dispatch) and then steals from the
 // others in turn: without stealing, a queue whose tiles were cheap left its
 // XCD idle while another XCD's queue ran 300-450 us longer (reflect_refract,
-// per-workgroup timestamps).  The heads are zeroed before every launch that
-// uses them, stream-ordered: by order_tiles on a cost-ordered pool launch,
-// by a memset otherwise (rtc_host.cpp launch), so their atomics need no
-// bookkeeping.
+// per-workgroup timestamps).  Every launch finds its heads zeroed (context
+// creation, then the previous dynamic launch: trace_pool), so their atomics
+// need no other bookkeeping.
 template <typename R>
-__device__ inline unsigned int next_tile(const LaunchParams<R>& P, uint32_t it, uint32_t& probe) {
+__device__ inline unsigned int next_tile(const LaunchParams<R>& P, uint32_t it, uint32_t& probe, uint32_t n_items) {
     if (P.persistent == kSchedGrid) return it == 0 ? blockIdx.x : 0xFFFFFFFFu;
     if (P.persistent == kSchedStatic) {
         const unsigned long long t = blockIdx.x + (unsigned long long)it * gridDim.x;
@@ -1017,7 +1016,7 @@ __device__ inline unsigned int next_tile(const LaunchParams<R>& P, uint32_t it, 
         const uint32_t q = (blockIdx.x + probe) % kTileQueues;
         const unsigned long long j = atomicAdd(&P.tile_counter[q * kQueueStride], 1ull);
         const unsigned long long i = q + (unsigned long long)kTileQueues * j;
-        if (i < P.n_tiles) return P.tile_order ? P.tile_order[i] : (unsigned int)i;
+        if (i < n_items) return P.tile_order ? P.tile_order[i] : (unsigned int)i;
     }
     return 0xFFFFFFFFu;
 }
@@ -1258,22 +1257,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
 
     Counts k = {};
     const uint32_t tid = threadIdx.x;
+    // Two sets of queue heads alternate between dynamic launches: this launch
+    // zeroes the set the next one uses (its last user, the previous launch,
+    // has completed: stream order).
+    if (P.persistent == kSchedDynamic && blockIdx.x == 0 && tid < (uint32_t)kTileQueues)
+        P.next_tile_counter[tid * kQueueStride] = 0ull;
     uint32_t probe = 0;
+    // thread 0: the items of this launch (read once: it sits on the dequeue path)
+    const uint32_t n_items = P.item_count && tid == 0 ? *P.item_count : P.n_tiles;
     unsigned long long tile_start = 0;  // thread 0: s_memrealtime at the tile's start
     for (uint32_t it = 0;; ++it) {
         if (tid == 0) {
-            s_tile[it & 1] = next_tile(P, it, probe);
+            s_tile[it & 1] = next_tile(P, it, probe, n_items);
             s_top[0] = 0;
             tile_start = __builtin_amdgcn_s_memrealtime();
         }
         for (int c = 0; c < 3; ++c) pl.acc[c * kBlock + tid] = 0;
         __syncthreads();
-        const uint32_t t = __builtin_amdgcn_readfirstlane(s_tile[it & 1]);
-        if (t >= P.n_tiles) break;
+        const uint32_t item = __builtin_amdgcn_readfirstlane(s_tile[it & 1]);
+        if (item == 0xFFFFFFFFu) break;
+        const uint32_t t = item & kItemTileMask, split = item >> kItemSplitShift;
         bool valid;
         V3<R> o, d;
         uint64_t out_idx;
         load_primary(P, t, tid, valid, o, d, out_idx);
+        // this item's part of the tile (all of it unless split)
+        valid &= ((tid >> 6) >> (2 - split)) == ((item >> kItemPartShift) & 3u);
         k.c[0] += wave_count(valid);
         {
             const int slot = wave_reserve(valid, &s_top[0]);
@@ -1324,8 +1333,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         __syncthreads();  // accumulators are re-zeroed for the next tile
         // this tile's cost (10 ns ticks) orders the next launch of the same
         // frame heaviest-first (order_tiles)
-        if (tid == 0 && P.tile_cost)
-            P.tile_cost[t] = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - tile_start, 0xFFFFFFFFull);
+        // (a split tile: its slowest part times the parts, order_tiles zeroed it)
+        if (tid == 0 && P.tile_cost) {
+            const uint32_t c = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - tile_start, 0x3FFFFFFFull);
+            if (split) atomicMax(&P.tile_cost[t], c << split);
+            else P.tile_cost[t] = c;
+        }
     }
     if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
     if (P.stamps) {
@@ -1335,13 +1348,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
 }
 
 #ifndef RTC_JIT  // the per-scene build (rtc_jit.cpp) holds the tracer kernels only
-// Heaviest-first tile order from the previous launch's per-tile costs: a
+// Heaviest-first work order from the previous launch's per-tile costs: a
 // one-workgroup bucket sort (8 buckets per octave of cost, descending).  The
 // pool kernel's time is set by its last, heaviest tiles (a glass-sphere tile
 // of reflect_refract runs ~400 us); handing those out first bounds the tail
 // (longest-processing-time-first).  Order within a bucket is arbitrary:
 // tiles are independent and pixel sums are fixed-point, so images are not
 // affected.
+//
+// A tile costing more than split_factor x the mean workgroup load (sum of
+// costs / grid) is handed out as 2 or 4 parts (items, rtc_internal.hpp): when
+// a launch has few tiles per workgroup (a shard of a multi-GPU frame) its
+// heaviest tiles outlast everything else, and the parts of one run on
+// different CUs.  The parts' seeds cover a quarter or half of the tile, and
+// its rays fill the pool within a few generations.  Split tiles' costs are
+// zeroed here and rebuilt by their parts (atomicMax of part cost x parts).
 constexpr int kOrderBuckets = 256;
 constexpr int kOrderThreads = 1024;
 
@@ -1350,18 +1371,39 @@ __device__ inline uint32_t cost_bucket(uint32_t c) {  // 0 = heaviest
     return (uint32_t)(kOrderBuckets - 1) - (b < (uint32_t)kOrderBuckets ? b : (uint32_t)(kOrderBuckets - 1));
 }
 
-// Also zeroes the dynamic schedule's queue heads, so a pool launch with a
-// tile order pays one small launch instead of a memset plus this kernel.
-__global__ __launch_bounds__(kOrderThreads) void order_tiles(const uint32_t* __restrict__ cost,
+// log2 of the parts a tile of cost c is split into (0, 1 or 2)
+__device__ inline uint32_t split_log2(uint32_t c, float limit) {
+    return (float)c > 2.0f * limit ? 2u : ((float)c > limit ? 1u : 0u);
+}
+
+__global__ __launch_bounds__(kOrderThreads) void order_tiles(uint32_t* __restrict__ cost,
                                                              uint32_t* __restrict__ order, uint32_t n,
-                                                             unsigned long long* __restrict__ heads,
-                                                             uint32_t n_heads) {
+                                                             uint32_t* __restrict__ n_items, float split_per_cost) {
     __shared__ uint32_t hist[kOrderBuckets];
     __shared__ uint32_t scan[kOrderBuckets];
-    for (uint32_t i = threadIdx.x; i < n_heads; i += kOrderThreads) heads[i] = 0ull;
+    __shared__ unsigned long long total;
+    __shared__ uint32_t items;
     for (uint32_t b = threadIdx.x; b < (uint32_t)kOrderBuckets; b += kOrderThreads) hist[b] = 0;
+    if (threadIdx.x == 0) {
+        total = 0;
+        items = 0;
+    }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) atomicAdd(&hist[cost_bucket(cost[i])], 1u);
+    float limit = __FLT_MAX__;  // split nothing
+    if (split_per_cost > 0.0f) {
+        unsigned long long mine = 0;
+        for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) mine += cost[i];
+        atomicAdd(&total, mine);
+        __syncthreads();
+        limit = (float)total * split_per_cost;
+    }
+    uint32_t mine_items = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) {
+        const uint32_t c = cost[i], l = split_log2(c, limit);
+        atomicAdd(&hist[cost_bucket(c >> l)], 1u << l);
+        mine_items += 1u << l;
+    }
+    atomicAdd(&items, mine_items);
     __syncthreads();
     // Exclusive scan of the 256 bucket counts: Hillis-Steele over LDS.
     const uint32_t t = threadIdx.x;
@@ -1380,7 +1422,13 @@ __global__ __launch_bounds__(kOrderThreads) void order_tiles(const uint32_t* __r
     }
     if (t < (uint32_t)kOrderBuckets) hist[t] = scan[t] - own;
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) order[atomicAdd(&hist[cost_bucket(cost[i])], 1u)] = i;
+    for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) {
+        const uint32_t c = cost[i], l = split_log2(c, limit);
+        const uint32_t pos = atomicAdd(&hist[cost_bucket(c >> l)], 1u << l);
+        for (uint32_t p = 0; p < (1u << l); ++p) order[pos + p] = i | p << kItemPartShift | l << kItemSplitShift;
+        if (l) cost[i] = 0;
+    }
+    if (threadIdx.x == 0) *n_items = items;
 }
 
 // De-interleave gathered shard strips into one image.
@@ -1505,10 +1553,10 @@ template hipError_t occupancy<float>(bool, bool, size_t, int*);
 template hipError_t launch_trace<double>(const LaunchParams<double>&, bool, bool, uint32_t, size_t, hipStream_t);
 template hipError_t occupancy<double>(bool, bool, size_t, int*);
 
-hipError_t launch_order_tiles(const uint32_t* cost, uint32_t* order, uint32_t n, unsigned long long* heads,
-                              uint32_t n_heads, hipStream_t stream) {
+hipError_t launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, uint32_t* n_items, float split_per_cost,
+                              hipStream_t stream) {
     (void)hipGetLastError();  // see launch_trace
-    hipLaunchKernelGGL(order_tiles, dim3(1), dim3(kOrderThreads), 0, stream, cost, order, n, heads, n_heads);
+    hipLaunchKernelGGL(order_tiles, dim3(1), dim3(kOrderThreads), 0, stream, cost, order, n, n_items, split_per_cost);
     return hipGetLastError();
 }
 

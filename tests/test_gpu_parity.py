@@ -231,6 +231,31 @@ def test_cost_ordered_schedule_is_exact(gpu_ctx, rtc, monkeypatch, name):
     assert np.array_equal(raster, first) and _counts(s0) == _counts(s1)
 
 
+@pytest.mark.parametrize("shard", [(0, 1), (1, 4)])
+@pytest.mark.parametrize("name", ["reflect_refract", "cover"])
+def test_split_tiles_are_exact(rtc, monkeypatch, name, shard):
+    """Heavy tiles handed out in 2 or 4 parts (order_tiles; RTC_SPLIT tiny
+    splits nearly every tile 4 ways, at 1 every tile above the mean load),
+    then the frozen order reused (launches 4 and 5): every render equals the
+    raster-ordered one bit for bit, counters included."""
+    scene = scene_fixture(name)
+    cam = rtc.camera_resize(scene.camera, 256, 160)
+    rows = rtc.shard_rows(cam.height, shard[1])
+    raster, s0 = _render_with_env(rtc, monkeypatch, {"RTC_TILE_ORDER": "0"}, scene, cam, "f32")
+    raster = raster[:rows] if shard[1] == 1 else None
+    for split in ("0.0001", "1"):
+        monkeypatch.setenv("RTC_TILE_ORDER", "1")
+        monkeypatch.setenv("RTC_SPLIT", split)
+        with rtc.Context(0) as c:
+            c.upload(scene)
+            first, s1 = c.render(cam, 6, precision="f32", shard=shard)
+            if raster is not None:
+                assert np.array_equal(first, raster) and _counts(s1) == _counts(s0)
+            for _ in range(4):
+                img, st = c.render(cam, 6, precision="f32", shard=shard)
+                assert np.array_equal(img, first) and _counts(st) == _counts(s1)
+
+
 @pytest.mark.parametrize("precision", ["f32", "f64"])
 def test_cull_is_exact_for_grazing_rays(gpu_ctx, rtc, monkeypatch, precision):
     """Rays aimed within 1e-6 of sphere and cube silhouettes (rt_color_at
