@@ -9,6 +9,7 @@
  *       scene_loader.rs:255-266, camera.rs:25-49/124-127,
  *       transformations.rs:75-87                      -> rt_camera_make
  *   Matrix<4>::inverse  primitives/matrix.rs:247-258  -> rt_matrix_inverse
+ *   Canvas::to_png_file / to_ppm  canvas.rs:75-137    -> rt_image_write
  * All arithmetic is f64 and follows the reference's operation order, so the
  * tables are bit-identical to what the reference holds after loading.
  * Pure host code: none of these functions needs a GPU.
@@ -63,6 +64,13 @@ int rt_camera_set_transform(rt_camera_desc* camera, const double transform[16]);
 
 /* Matrix<4>::inverse, row-major 16 doubles. */
 int rt_matrix_inverse(const double m[16], double out[16]);
+
+/* Canvas::to_png_file / to_ppm (canvas.rs:75-137) for an 8-bit frame
+ * (rt_render with RT_OUT_U8, row-major RGB, y = 0 at the top): a path ending
+ * in ".png" (any case) gets an RGB8 PNG (filter None, best deflate, as the
+ * reference writes), anything else a binary PPM (P6).  RT_ERR_IO on a write
+ * failure.  Host only. */
+int rt_image_write(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height);
 
 #ifdef __cplusplus
 }

@@ -2,8 +2,9 @@
 // (`<SCENE> <OUT> [-q]`, timing of the render call only, main.rs:17-24) for the
 // GPU render path.  Extra flags: --width/--height (same as editing the YAML
 // camera size), --depth (World::MAX_REFLECTION_ITERATIONS = 6 by default),
-// --precision f32|f64, --device N.  Writes a binary PPM (P6) quantized as
-// canvas.rs:117-123 does.
+// --precision f32|f64, --device N.  Writes OUT as PNG when it ends in .png
+// (canvas.rs:114-137, as the reference CLI does), a binary PPM (P6)
+// otherwise; pixels quantized on the device as canvas.rs:117-123 does.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -16,7 +17,7 @@
 
 static int usage() {
     std::fprintf(stderr,
-                 "usage: rtc <SCENE.yaml> <OUT.ppm> [-q] [--width W] [--height H] [--depth D]\n"
+                 "usage: rtc <SCENE.yaml> <OUT.png|OUT.ppm> [-q] [--width W] [--height H] [--depth D]\n"
                  "           [--precision f32|f64] [--device N]\n");
     return 2;
 }
@@ -75,14 +76,10 @@ int main(int argc, char** argv) {
                     (unsigned long long)st.primary, (unsigned long long)st.shadow, (unsigned long long)st.reflect,
                     (unsigned long long)st.refract, rays / (st.kernel_ms * 1e3));
     }
-    FILE* f = std::fopen(out_path, "wb");
-    if (!f) {
-        std::fprintf(stderr, "error: cannot write %s\n", out_path);
+    if (rt_image_write(out_path, img.data(), cam.width, cam.height) != RT_OK) {
+        std::fprintf(stderr, "error: %s\n", rt_last_error());
         return 1;
     }
-    std::fprintf(f, "P6\n%u %u\n255\n", cam.width, cam.height);
-    std::fwrite(img.data(), 1, img.size(), f);
-    std::fclose(f);
     if (!quiet) std::printf("Image saved to: %s\n", out_path);
     rt_context_destroy(ctx);
     rt_scene_free(scene);

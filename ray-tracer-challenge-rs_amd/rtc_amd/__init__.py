@@ -167,6 +167,7 @@ def _load() -> C.CDLL:
         "rt_scene_load_yaml_text": (C.c_int, [C.c_char_p, P(C.c_void_p)]),
         "rt_scene_view_get": (C.c_int, [C.c_void_p, P(SceneView)]),
         "rt_scene_free": (None, [C.c_void_p]),
+        "rt_image_write": (C.c_int, [C.c_char_p, C.c_void_p, C.c_uint32, C.c_uint32]),
         "rt_camera_make": (C.c_int, [C.c_uint32, C.c_uint32, C.c_double, P(C.c_double), P(C.c_double),
                                      P(C.c_double), P(CameraDesc)]),
         "rt_camera_resize": (C.c_int, [P(CameraDesc), C.c_uint32, C.c_uint32]),
@@ -203,7 +204,7 @@ EXPORTED_SYMBOLS = (
     "rt_shard_row_map", "rt_context_create_multi", "rt_comm_unique_id", "rt_context_create_rank", "rt_context_group",
     "rt_context_set_jit", "rt_jit_status",
     "rt_assemble_shards", "rt_scene_load_yaml", "rt_scene_load_yaml_text", "rt_scene_view_get", "rt_scene_free",
-    "rt_camera_make", "rt_camera_resize", "rt_matrix_inverse",
+    "rt_camera_make", "rt_camera_resize", "rt_matrix_inverse", "rt_image_write",
 )
 
 
@@ -251,6 +252,15 @@ def camera_resize(cam: CameraDesc, width: int, height: int) -> CameraDesc:
     c = cam.copy()
     _check(_lib.rt_camera_resize(C.byref(c), width, height))
     return c
+
+
+def write_image(path, image: np.ndarray) -> None:
+    """Canvas::to_png_file / to_ppm (canvas.rs:75-137) of an 8-bit (H, W, 3) frame
+    (render(..., out_format="u8")): PNG when `path` ends in .png, binary PPM otherwise."""
+    img = np.ascontiguousarray(image)
+    if img.dtype != np.uint8 or img.ndim != 3 or img.shape[2] != 3:
+        raise ValueError("write_image takes a uint8 array of shape (H, W, 3)")
+    _check(_lib.rt_image_write(os.fsencode(path), img.ctypes.data, img.shape[1], img.shape[0]))
 
 
 def shard_rows(height: int, shard_count: int) -> int:
