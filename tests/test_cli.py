@@ -74,3 +74,21 @@ def test_cli_renders_the_scene_like_the_oracle(tmp_path, rtc, oracle):
     ref, _ = oracle.render(scene, rtc.camera_resize(scene.camera, 80, 60), 6)
     d = np.abs(img.astype(int) - oracle.quantize(ref).astype(int))
     assert d.max() <= 1 and (d == 0).mean() >= 0.999
+
+
+@pytest.mark.gpu
+def test_cli_png_equals_ppm(tmp_path):
+    """`rtc scene.yaml out.png` saves the same pixels as PNG (main.rs:26,
+    canvas.rs:114-137) that `out.ppm` saves as PPM."""
+    PIL = pytest.importorskip("PIL.Image")
+    yaml = tmp_path / "scene.yaml"
+    yaml.write_text(SCENE)
+    outs = {}
+    for ext in ("ppm", "png"):
+        out = tmp_path / f"out.{ext}"
+        r = subprocess.run([CLI, str(yaml), str(out), "-q", "--width", "64", "--height", "48"],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        outs[ext] = out
+    with PIL.open(outs["png"]) as im:
+        assert np.array_equal(np.asarray(im.convert("RGB")), read_ppm(outs["ppm"]))
