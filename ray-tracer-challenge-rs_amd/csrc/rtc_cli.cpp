@@ -1,10 +1,15 @@
 // rtc_cli.cpp — command-line driver mirroring ray-tracer-cli/src/main.rs:11-31
-// (`<SCENE> <OUT> [-q]`, timing of the render call only, main.rs:17-24) for the
-// GPU render path.  Extra flags: --width/--height (same as editing the YAML
-// camera size), --depth (World::MAX_REFLECTION_ITERATIONS = 6 by default),
-// --precision f32|f64, --device N.  Writes OUT as PNG when it ends in .png
-// (canvas.rs:114-137, as the reference CLI does), a binary PPM (P6)
-// otherwise; pixels quantized on the device as canvas.rs:117-123 does.
+// and cli/cli_arguments.rs:4-13: `<SCENE> <OUT> [-r serial|parallel] [-q]`,
+// timing of the render call only (main.rs:17-24), then the PNG save
+// (main.rs:26, canvas.rs:114-137; OUT ending in anything but .png gets a
+// binary PPM).  The reference's rendering modes pick Camera::render or
+// render_parallel; here every mode renders on the GPU (the library owns the
+// parallelism), so `-r serial|parallel|gpu` are accepted and equivalent.
+// Extra flags: --width/--height (same as editing the YAML camera size),
+// --depth (World::MAX_REFLECTION_ITERATIONS = 6 by default), --precision
+// f32|f64, --device N, --gpus N (split the frame across devices 0..N-1 of a
+// multi-GPU context).  Pixels are quantized on the device as
+// canvas.rs:117-123 does.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -17,8 +22,8 @@
 
 static int usage() {
     std::fprintf(stderr,
-                 "usage: rtc <SCENE.yaml> <OUT.png|OUT.ppm> [-q] [--width W] [--height H] [--depth D]\n"
-                 "           [--precision f32|f64] [--device N]\n");
+                 "usage: rtc <SCENE.yaml> <OUT.png|OUT.ppm> [-r serial|parallel|gpu] [-q] [--width W] [--height H]\n"
+                 "           [--depth D] [--precision f32|f64] [--device N] [--gpus N]\n");
     return 2;
 }
 
@@ -28,11 +33,16 @@ int main(int argc, char** argv) {
     const char* out_path = argv[2];
     bool quiet = false;
     uint32_t width = 0, height = 0, depth = RT_DEFAULT_MAX_DEPTH, precision = RT_PRECISION_F32;
-    int device = 0;
+    int device = 0, gpus = 1;
     for (int i = 3; i < argc; ++i) {
         std::string a = argv[i];
         auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : nullptr; };
         if (a == "-q" || a == "--quiet") quiet = true;
+        else if (a == "-r" || a == "--rendering-mode") {
+            const char* v = next();
+            if (!v || (std::strcmp(v, "serial") && std::strcmp(v, "parallel") && std::strcmp(v, "gpu"))) return usage();
+        }
+        else if (a == "--gpus") { const char* v = next(); if (!v || std::atoi(v) < 1) return usage(); gpus = std::atoi(v); }
         else if (a == "--width") { const char* v = next(); if (!v) return usage(); width = (uint32_t)std::atoi(v); }
         else if (a == "--height") { const char* v = next(); if (!v) return usage(); height = (uint32_t)std::atoi(v); }
         else if (a == "--depth") { const char* v = next(); if (!v) return usage(); depth = (uint32_t)std::atoi(v); }
@@ -43,7 +53,7 @@ int main(int argc, char** argv) {
             precision = std::strcmp(v, "f64") == 0 ? RT_PRECISION_F64 : RT_PRECISION_F32;
         } else return usage();
     }
-    if (!quiet) std::printf("Rendering scene: %s\n", scene_path);
+    if (!quiet) std::printf("Rendering image using scene at %s\n", scene_path);
     rt_scene* scene = nullptr;
     if (rt_scene_load_yaml(scene_path, &scene) != RT_OK) {
         std::fprintf(stderr, "error: %s\n", rt_last_error());
@@ -54,7 +64,10 @@ int main(int argc, char** argv) {
     rt_camera_desc cam = v.camera;
     if (width || height) rt_camera_resize(&cam, width ? width : cam.width, height ? height : cam.height);
     rt_context* ctx = nullptr;
-    if (rt_context_create(device, &ctx) != RT_OK ||
+    std::vector<int> devices;
+    for (int g = 0; g < gpus; ++g) devices.push_back(device + g);
+    const int created = gpus > 1 ? rt_context_create_multi(devices.data(), gpus, &ctx) : rt_context_create(device, &ctx);
+    if (created != RT_OK ||
         rt_scene_upload(ctx, v.shapes, v.n_shapes, v.materials, v.n_materials, v.patterns, v.n_patterns, v.lights,
                         v.n_lights) != RT_OK) {
         std::fprintf(stderr, "error: %s\n", rt_last_error());
@@ -70,7 +83,8 @@ int main(int argc, char** argv) {
     }
     double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (!quiet) {
-        std::printf("Image rendered in: %.3fs (kernel %.3f ms)\n", s, st.kernel_ms);
+        std::printf("Image rendered in: %.3fs\n", s);
+        std::printf("kernel %.3f ms on %u GPU(s)\n", st.kernel_ms, st.n_shards ? st.n_shards : 1u);
         const double rays = (double)(st.primary + st.shadow + st.reflect + st.refract);
         std::printf("rays: primary %llu shadow %llu reflect %llu refract %llu (%.1f Mray/s kernel)\n",
                     (unsigned long long)st.primary, (unsigned long long)st.shadow, (unsigned long long)st.reflect,
@@ -80,7 +94,7 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "error: %s\n", rt_last_error());
         return 1;
     }
-    if (!quiet) std::printf("Image saved to: %s\n", out_path);
+    if (!quiet) std::printf("Image saved at %s\n", out_path);
     rt_context_destroy(ctx);
     rt_scene_free(scene);
     return 0;

@@ -56,6 +56,7 @@ def read_ppm(path):
 
 def test_cli_usage_and_missing_scene_fail_loudly(tmp_path):
     assert subprocess.run([CLI], capture_output=True).returncode != 0
+    assert subprocess.run([CLI, "a.yaml", "b.png", "-r", "bogus"], capture_output=True).returncode == 2
     r = subprocess.run([CLI, str(tmp_path / "missing.yaml"), str(tmp_path / "o.ppm")], capture_output=True, text=True)
     assert r.returncode != 0 and "error" in r.stderr
 
@@ -84,11 +85,12 @@ def test_cli_png_equals_ppm(tmp_path):
     yaml = tmp_path / "scene.yaml"
     yaml.write_text(SCENE)
     outs = {}
-    for ext in ("ppm", "png"):
+    for ext, mode in (("ppm", "parallel"), ("png", "serial")):  # the reference's -r modes: same GPU render
         out = tmp_path / f"out.{ext}"
-        r = subprocess.run([CLI, str(yaml), str(out), "-q", "--width", "64", "--height", "48"],
+        r = subprocess.run([CLI, str(yaml), str(out), "-r", mode, "--width", "64", "--height", "48"],
                            capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr
+        assert f"Image saved at {out}" in r.stdout  # main.rs:27-29
         outs[ext] = out
     with PIL.open(outs["png"]) as im:
         assert np.array_equal(np.asarray(im.convert("RGB")), read_ppm(outs["ppm"]))
