@@ -2,7 +2,7 @@
 """Diagnostic: which frames run a per-scene kernel (rt_jit_status) and, with
 RTC_JIT_DUMP=<dir>, the generated scene headers and code objects.
 
-Usage: jit_report.py [scene[:WxH] ...]
+Usage: [JIT_PRECISION=f64] jit_report.py [scene[:WxH] ...]
 """
 import os
 import sys
@@ -24,10 +24,11 @@ def main():
         cam = rtc_amd.camera_resize(scene.camera, w, h)
         with rtc_amd.Context(0) as ctx:
             ctx.upload(scene)
-            out = torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
-            ctx.render_device(cam, out.data_ptr(), 0, 6, "f32")
+            prec = os.environ.get("JIT_PRECISION", "f32")
+            out = torch.empty((h, w, 3), dtype=torch.float32 if prec == "f32" else torch.float64, device="cuda")
+            ctx.render_device(cam, out.data_ptr(), 0, 6, prec)
             torch.cuda.synchronize()
-            print(name, f"{w}x{h}", ctx.jit_status(), flush=True)
+            print(name, f"{w}x{h}", prec, ctx.jit_status(), flush=True)
 
 
 if __name__ == "__main__":
