@@ -71,3 +71,33 @@ def test_group_upload_errors_are_reported(group_ctx, rtc):
         group_ctx.upload(bad)
     with pytest.raises(rtc.RenderError):  # nothing uploaded yet
         group_ctx.render(rtc.camera_resize(bad.camera, 8, 8), 6)
+
+
+def test_group_back_to_back_frames(gpu_ctx, group_ctx, rtc):
+    """Back-to-back render_device calls with nothing in between, of
+    alternating cameras, sizes and formats into separate outputs on a torch
+    side stream (strip and gather buffers reused and resized between frames):
+    each must equal the single-GPU frame, and a host-path render queued right
+    after must see its own frame."""
+    import torch
+    scene = scene_fixture("reflect_refract")
+    group_ctx.upload(scene)
+    gpu_ctx.upload(scene)
+    cams = [rtc.camera_resize(scene.camera, 320, 180), rtc.camera_resize(scene.camera, 256, 200)]
+    view = np.linalg.inv(np.array(list(cams[0].inverse)).reshape(4, 4))
+    shift = np.array([[1, 0, 0, 0.3], [0, 1, 0, -0.2], [0, 0, 1, 0.5], [0, 0, 0, 1.0]])
+    moved = rtc.camera_set_transform(cams[0], shift @ view)
+    jobs = [(cams[0], "real"), (cams[1], "u8"), (moved, "real"), (cams[1], "real"), (cams[0], "u8"), (moved, "u8")]
+    refs = [gpu_ctx.render(c, 6, precision="f32", out_format=f)[0] for c, f in jobs]
+    side = torch.cuda.Stream()
+    outs = []
+    with torch.cuda.stream(side):
+        for c, f in jobs:
+            o = torch.zeros((c.height, c.width, 3), dtype=torch.uint8 if f == "u8" else torch.float32, device="cuda")
+            group_ctx.render_device(c, o.data_ptr(), side.cuda_stream, 6, "f32", f)
+            outs.append(o)
+    host, _ = group_ctx.render(cams[1], 6, precision="f32")
+    side.synchronize()
+    for (c, f), o, r in zip(jobs, outs, refs):
+        assert np.array_equal(o.cpu().numpy(), r), (c.width, c.height, f)
+    assert np.array_equal(host, refs[3])
