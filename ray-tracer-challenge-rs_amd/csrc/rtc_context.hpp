@@ -87,7 +87,9 @@ struct rt_context {
     uint32_t* d_tile_order = nullptr;
     uint32_t order_capacity = 0;
     uint64_t order_sig = 0;
+    uint64_t order_geometry = 0;  // order_sig without the camera
     bool order_valid = false;
+    bool order_built = false;     // d_tile_order holds an order for order_geometry
     // Tiles costing more than split_factor x the mean workgroup load are
     // handed out in parts (order_tiles); RTC_SPLIT=0 never splits.
     double split_factor = 1.5;

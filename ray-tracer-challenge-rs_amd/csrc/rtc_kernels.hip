@@ -1389,21 +1389,28 @@ __global__ __launch_bounds__(kOrderThreads) void order_tiles(uint32_t* __restric
         items = 0;
     }
     __syncthreads();
+    // wave sums first: 1024 same-address LDS atomics serialized to ~8 us
+    auto wave_sum = [](unsigned long long v) {
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        return v;
+    };
     float limit = __FLT_MAX__;  // split nothing
     if (split_per_cost > 0.0f) {
         unsigned long long mine = 0;
         for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) mine += cost[i];
-        atomicAdd(&total, mine);
+        mine = wave_sum(mine);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&total, mine);
         __syncthreads();
         limit = (float)total * split_per_cost;
     }
-    uint32_t mine_items = 0;
+    unsigned long long mine_items = 0;
     for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) {
         const uint32_t c = cost[i], l = split_log2(c, limit);
         atomicAdd(&hist[cost_bucket(c >> l)], 1u << l);
         mine_items += 1u << l;
     }
-    atomicAdd(&items, mine_items);
+    mine_items = wave_sum(mine_items);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&items, (uint32_t)mine_items);
     __syncthreads();
     // Exclusive scan of the 256 bucket counts: Hillis-Steele over LDS.
     const uint32_t t = threadIdx.x;

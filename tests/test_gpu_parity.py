@@ -404,3 +404,29 @@ def test_consecutive_launches_keep_queue_epochs(gpu_ctx, rtc):
                     else:
                         assert np.array_equal(img, first[key][0]) and _counts(st) == first[key][1], key
                     assert st["primary"] == cam.width * cam.height
+
+
+@pytest.mark.parametrize("name", ["reflect_refract", "cover"])
+def test_moved_camera_reuses_order_exactly(gpu_ctx, rtc, monkeypatch, name):
+    """A moved camera starts from the previous camera's tile order (plan_tile_order):
+    scheduling only — every frame along the path equals its raster-ordered render."""
+    scene = scene_fixture(name)
+    base = rtc.camera_resize(scene.camera, 256, 160)
+    view = np.linalg.inv(np.array(list(base.inverse)).reshape(4, 4))
+    cams = []
+    for k in range(3):
+        shift = np.eye(4)
+        shift[0, 3] = 0.05 * k
+        cams.append(rtc.camera_set_transform(base, shift @ view))
+    gpu_ctx.upload(scene)
+    ordered = []
+    for c in cams:
+        for _ in range(3):  # the last two launches of each camera run an order built for it
+            img, st = gpu_ctx.render(c, 6, precision="f32")
+        ordered.append((img, st))
+    monkeypatch.setenv("RTC_TILE_ORDER", "0")
+    with rtc.Context(0) as raster_ctx:
+        raster_ctx.upload(scene)
+        for c, (img, st) in zip(cams, ordered):
+            ref, sr = raster_ctx.render(c, 6, precision="f32")
+            assert np.array_equal(img, ref) and _counts(st) == _counts(sr)
