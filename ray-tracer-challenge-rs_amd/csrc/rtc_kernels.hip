@@ -443,11 +443,15 @@ __device__ inline bool wave_may_hit(const ShapeRec<R>& s, V3<R> o, V3<R> d) {
 // top of each unrolled shape, so the compiler cannot hoist every shape's
 // ray-dependent terms (the cull's |o - c|^2, ...) to the front of the
 // unrolled sequence, where they stay live and spill.  A no-op otherwise.
+#ifndef RTC_JIT_FENCE_EVERY
+#define RTC_JIT_FENCE_EVERY 1
+#endif
 template <typename R>
-__device__ inline void jit_fence(V3<R>& o, V3<R>& d) {
+__device__ inline void jit_fence(V3<R>& o, V3<R>& d, int slot = 0) {
 #if defined(RTC_JIT) && !defined(RTC_JIT_NO_FENCE)
     if constexpr (sizeof(R) == 4)
-        asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z), "+v"(d.x), "+v"(d.y), "+v"(d.z));
+        if (slot % RTC_JIT_FENCE_EVERY == 0)
+            asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z), "+v"(d.x), "+v"(d.y), "+v"(d.z));
 #endif
 }
 
@@ -511,7 +515,7 @@ template <typename R>
 __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
     Nearest<R> best;
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
-        jit_fence(o, d);
+        jit_fence(o, d, slot);
         if (!wave_may_hit<R, K>(s, o, d)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
@@ -551,7 +555,7 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) 
     Blocker<R> b;
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
         if (!s.casts_shadow) return;  // wave-uniform
-        jit_fence(o, d);
+        jit_fence(o, d, slot);
         if (!wave_may_hit<R, K>(s, o, d)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
