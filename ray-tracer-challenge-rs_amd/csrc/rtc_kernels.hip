@@ -48,10 +48,17 @@ namespace RTC_VARIANT {
 template <typename R>
 struct Real;
 
+// RTC_F32_EXACT / RTC_F32_OFFSET: builds for the f32 error study
+// (tests/study_f32_error.py) — correctly rounded division,
+// square root and pow instead of the hardware approximations, and another
+// over/under-point offset.  The product build uses neither.
+#ifndef RTC_F32_OFFSET
+#define RTC_F32_OFFSET 1e-4f
+#endif
 template <>
 struct Real<float> {
     static constexpr float kEps = 8e-8f;        // guards (consts.rs:2)
-    static constexpr float kOffset = 1e-4f;     // over/under point + cap normals:
+    static constexpr float kOffset = RTC_F32_OFFSET;  // over/under point + cap normals:
                                                 // 8e-8 is below the f32 ulp at |p|>0.7
     static constexpr float kMax = __FLT_MAX__;  // consts.rs:8 analogue
     static constexpr float kInf = __builtin_huge_valf();
@@ -59,12 +66,19 @@ struct Real<float> {
     __device__ static inline float madd(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
     // reference `mul_add` sites
     __device__ static inline float rfma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+#ifdef RTC_F32_EXACT
+    __device__ static inline float div(float a, float b) { return a / b; }
+    __device__ static inline float sqrt(float a) { return __builtin_sqrtf(a); }
+    __device__ static inline float rsqrt(float a) { return 1.0f / __builtin_sqrtf(a); }
+    __device__ static inline float pow(float x, float y) { return __builtin_powf(x, y); }
+#else
     __device__ static inline float div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
     __device__ static inline float sqrt(float a) { return __builtin_amdgcn_sqrtf(a); }
     __device__ static inline float rsqrt(float a) { return __builtin_amdgcn_rsqf(a); }
     __device__ static inline float pow(float x, float y) {  // x in (0, 1] here
         return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
     }
+#endif
     __device__ static inline float floor(float a) { return __builtin_floorf(a); }
     __device__ static inline float trunc(float a) { return __builtin_truncf(a); }
     __device__ static inline float fabs(float a) { return __builtin_fabsf(a); }
