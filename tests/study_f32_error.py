@@ -1,16 +1,21 @@
 #!/usr/bin/env python3
 """Study (not collected by pytest): where does the f32 path's error against
 the f64 oracle come from?  Renders scenes at 320x200 with library builds
-that differ only in the f32 math (csrc/rtc_kernels.hip Real<float>):
-  default      hardware rcp/sqrt/exp/log approximations, offset 1e-4
-  exact        correctly rounded division, sqrt and pow (RTC_F32_EXACT)
-  off1e5/1e3   over/under-point offset 1e-5 / 1e-3 (RTC_F32_OFFSET)
-and reports, per scene, the share of pixels within 2/255 of the oracle
-after 8-bit quantization, the mean |err| and the ray-count drift.
-Frames of 64K pixels or fewer run the generic kernels (no per-scene build).
+that differ only in the f32 math (csrc/rtc_kernels.hip Real<float>) and
+reports, per scene, the share of pixels within 2/255 of the oracle after
+8-bit quantization, the mean |err| and the ray-count drift.  Frames of 64K
+pixels or fewer run the generic kernels (no per-scene build).
 
-Usage: python tests/study_f32_error.py [scene ...]   (on a GPU box; builds under
-ray-tracer-challenge-rs_amd/rtc_amd/_lib_<variant>/)
+Variants are library builds under ray-tracer-challenge-rs_amd/rtc_amd/_lib_<name>/,
+made with the Makefile's OUT and EXTRA, e.g.
+  make -C ray-tracer-challenge-rs_amd OUT=rtc_amd/_lib_exact EXTRA=-DRTC_F32_EXACT=1 \
+       rtc_amd/_lib_exact/librtc.so
+  (RTC_F32_EXACT: correctly rounded div/sqrt/pow; RTC_F32_REL_OFFSET=<x>f: the
+  over/under-point offset x * max(1, |p|inf))
+"default" is the product build (_lib).  The results are in DESIGN.md §4.
+
+Usage: STUDY_VARIANTS="default exact ..." python tests/study_f32_error.py [scene ...]
+(on a GPU box)
 """
 import json
 import os
@@ -20,7 +25,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIBS = os.path.join(ROOT, "ray-tracer-challenge-rs_amd", "rtc_amd")
-VARIANTS = ["default", "exact", "off1e5", "off1e3", "exactoff1e5"]
+VARIANTS = os.environ.get("STUDY_VARIANTS", "default").split()
 SCENES = ["refraction", "reflect_refract", "cover", "table", "shadow_puppets"]
 
 

@@ -10,7 +10,8 @@ Tolerances (the f64 -> f32 statement of DESIGN.md §Parity):
     F32_MEAN and ray counters within F32_RAYS relative.  Residual mismatches
     sit on silhouettes, shadow terminators and pattern edges where an f32
     rounding flips a branch, and f32 needs its own over/under-point offset
-    (1e-4 instead of 8e-8, which is below the f32 ulp at |p| > 0.7).
+    (3e-5 x max(1, |p|inf) instead of 8e-8, which is below the f32 ulp at
+    |p| > 0.7; DESIGN.md §4 has the study that chose it).
 """
 import math
 
@@ -23,13 +24,14 @@ pytestmark = pytest.mark.gpu
 
 ABS64 = 1e-9
 F32_PIX_FRAC = 0.99
-F32_MEAN = 2e-3
+F32_MEAN = 1e-3
 F32_RAYS = 0.01       # total rays per frame
 F32_RAYS_KIND = 0.05  # each ray kind (TIR / near-coincident faces flip single spawns)
 # refraction.yaml is a glass ball lens over a checker plane: rays bounce up to
-# 6 times inside the ball and the lens magnifies f32 direction error onto
-# checker edges.
-F32_SCENE_FLOOR = {"refraction": (0.95, 6e-3)}
+# 6 times inside the ball and the lens magnifies the f32 over/under-point
+# offset's departure from the reference's 8e-8 onto checker edges (DESIGN.md
+# §4: 97.6 % within 2/255 at 320x200; 95.5 % with round 1's fixed 1e-4).
+F32_SCENE_FLOOR = {"refraction": (0.97, 3e-3)}
 SQ2 = math.sqrt(2.0)
 
 SCENES = ["three_sphere_scene", "reflect_refract", "cover", "table", "cylinders", "metal", "refraction",
