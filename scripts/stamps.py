@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--out", default="real", choices=["real", "u8"])
+    ap.add_argument("--shard", default="0/1", help="shard_index/shard_count")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -34,9 +35,11 @@ def main():
     ctx = rtc_amd.Context(0)
     ctx.upload(scene)
     dt = torch.uint8 if args.out == "u8" else (torch.float32 if args.precision == "f32" else torch.float64)
-    out = torch.empty((cam.height, cam.width, 3), dtype=dt, device="cuda")
+    si, sn = map(int, args.shard.split("/"))
+    rows = rtc_amd.shard_rows(cam.height, sn)
+    out = torch.empty((rows, cam.width, 3), dtype=dt, device="cuda")
     for _ in range(5):
-        ctx.render_device(cam, out.data_ptr(), 0, 6, args.precision, args.out, (0, 1), args.flags | 8)
+        ctx.render_device(cam, out.data_ptr(), 0, 6, args.precision, args.out, (si, sn), args.flags | 8)
     torch.cuda.synchronize()
     st = ctx.debug_stamps().astype(np.int64)
     t0 = st[:, 0].min()
@@ -48,7 +51,7 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     ev[0].record()
     for _ in range(50):
-        ctx.render_device(cam, out.data_ptr(), 0, 6, args.precision, args.out, (0, 1), args.flags)
+        ctx.render_device(cam, out.data_ptr(), 0, 6, args.precision, args.out, (si, sn), args.flags)
     ev[1].record()
     torch.cuda.synchronize()
     res = {"label": f"{args.scene} flags={args.flags} out={args.out} sched={os.environ.get('RTC_SCHED_DIRECT', 'default')}",
