@@ -1020,12 +1020,24 @@ __device__ inline void load_primary(const LaunchParams<R>& P, uint32_t t, uint32
     }
 }
 
-// Lane 0 adds the wave's (uniform) counters into the wave's counter shard.
+// The workgroup's counters into its counter shard: each wave's lane 0 puts
+// the wave's (uniform) counts in LDS, and after one barrier lanes 0..7 of
+// wave 0 add the workgroup's sums, one atomic each.  (Every wave adding its
+// own eight, one after another, cost 0.8 us of a 23.6 us three_sphere frame:
+// the last waves' atomics sit on the kernel's tail.)  Called by every thread
+// of the workgroup.
 __device__ inline void flush_counts(const Counts& k, unsigned long long* global) {
-    const uint32_t shard = (blockIdx.x * (kBlock / 64) + threadIdx.x / 64) % kCounterShards;
-    if ((threadIdx.x & 63) == 0)
-        for (int i = 0; i < kNumCounters; ++i)
-            if (k.c[i]) atomicAdd(&global[shard * kNumCounters + i], (unsigned long long)k.c[i]);
+    __shared__ uint32_t s_counts[kBlock / 64][kNumCounters];
+    const uint32_t wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+    if (lane == 0)
+        for (int i = 0; i < kNumCounters; ++i) s_counts[wave][i] = k.c[i];
+    __syncthreads();
+    if (threadIdx.x < (uint32_t)kNumCounters) {
+        unsigned long long v = 0;
+        for (uint32_t w = 0; w < kBlock / 64; ++w) v += s_counts[w][threadIdx.x];
+        const uint32_t shard = blockIdx.x % kCounterShards;
+        if (v) atomicAdd(&global[shard * kNumCounters + threadIdx.x], v);
+    }
 }
 
 // Next work item of this workgroup (called by thread 0 only; `probe` lives in
