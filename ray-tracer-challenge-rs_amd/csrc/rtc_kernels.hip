@@ -971,14 +971,14 @@ __device__ inline void store_pixel(const LaunchParams<R>& P, uint64_t idx, V3<R>
             else return (uint8_t)__builtin_round(v * (R)255);
         };
         uint8_t* o = static_cast<uint8_t*>(P.out) + 3 * idx;
-        o[0] = q(c.x);
-        o[1] = q(c.y);
-        o[2] = q(c.z);
+        __builtin_nontemporal_store(q(c.x), o);
+        __builtin_nontemporal_store(q(c.y), o + 1);
+        __builtin_nontemporal_store(q(c.z), o + 2);
     } else {
         R* o = static_cast<R*>(P.out) + 3 * idx;
-        o[0] = c.x;
-        o[1] = c.y;
-        o[2] = c.z;
+        __builtin_nontemporal_store(c.x, o);
+        __builtin_nontemporal_store(c.y, o + 1);
+        __builtin_nontemporal_store(c.z, o + 2);
     }
 }
 
