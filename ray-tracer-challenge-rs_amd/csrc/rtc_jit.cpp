@@ -216,15 +216,15 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
     }
     // The launch is planned with the generic kernel's occupancy: use the
     // per-scene kernel only if it keeps at least as many workgroups per CU,
-    // and only if it spills at most one or two values (direct: none; pool:
-    // 8 B/lane, e.g. cylinders' pixel mapping, read once per tile: 0.161 ms
-    // against 0.189 ms for the generic kernel).  A build with real spills
-    // ran slower than the generic kernel (shadow_puppets before the ray
-    // fence: 56 B/lane, +10 %).
+    // and only if it spills at most a few values (direct: none; pool:
+    // 16 B/lane, e.g. cylinders: 12 B/lane, values reloaded once per tile,
+    // 0.15 ms against 0.19 ms for the generic kernel).  A build with real
+    // spills ran slower than the generic kernel (shadow_puppets before the
+    // ray fence: 56 B/lane, +10 %).
     int blocks = 0, scratch = 0;
     RT_HIP(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mf.second, kBlock, dyn_lds));
     RT_HIP(hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, mf.second));
-    if (blocks < static_blocks || scratch > (pool ? 8 : 0)) {
+    if (blocks < static_blocks || scratch > (pool ? 16 : 0)) {
         ctx->jit_failed = true;
         ctx->jit_log = "per-scene kernel not used: " + std::to_string(blocks) + " workgroups/CU (generic " +
                        std::to_string(static_blocks) + "), " + std::to_string(scratch) + " B/lane of scratch";
