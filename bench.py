@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--warmup-ms", type=float, default=200.0,
+                    help="keep warming up (untimed) until at least this much wall time of frames has run, "
+                         "whatever --warmup: a few 25 us frames leave the GPU below its steady clocks")
     ap.add_argument("--mode", choices=["auto", "frames", "tiled"], default="auto",
                     help="auto: one GPU renders frames; N > 1 GPUs split each frame (tiled)")
     ap.add_argument("--scene", default=None,
@@ -121,15 +124,24 @@ def load_traffic(workload: str):
 
 
 def timed_launches(fn, stream, n):
-    """Device milliseconds of n back-to-back calls of fn(), one event pair on `stream`."""
+    """Device milliseconds of n back-to-back calls of fn(), one event pair on `stream`.
+    The events are created (torch makes the HIP event at its first record) and
+    recorded once before the caller's clock starts: a lazy hipEventCreate inside
+    a 20-frame region added ~70 us to it (scripts/short_region_probe.py)."""
     import torch
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
-    for _ in range(n):
-        fn()
     e1.record(stream)
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1)
+
+    def run():
+        e0.record(stream)
+        for _ in range(n):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1)
+    return run
 
 
 def main():
@@ -195,9 +207,25 @@ def main():
     step()  # first frame: scene transfer, context, upload and one render
     torch.cuda.synchronize()
     first_frame_ms = (time.perf_counter() - t_first) * 1e3
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
+    # W untimed steps, continued (still untimed) until --warmup-ms of frames
+    # have run: on MI355X a 1080p frame after 5 warm-up frames takes 24.6 us
+    # against 22.8 us in steady state (scripts/steps_probe.sh), the clocks
+    # still ramping.  Every rank runs the same count (max over ranks).
+    warm_run = 0
+    t_w = time.perf_counter()
+    while True:
+        n = max(1, args.warmup - warm_run) if warm_run < args.warmup else max(1, warm_run)
+        for _ in range(n):
+            step()
+        warm_run += n
+        torch.cuda.synchronize()
+        done = warm_run >= args.warmup and (time.perf_counter() - t_w) * 1e3 >= args.warmup_ms
+        if world > 1:
+            flag = torch.tensor([0 if done else 1], dtype=torch.int32)
+            dist.all_reduce(flag)  # gloo, host tensor: continue while any rank wants to
+            done = int(flag.item()) == 0
+        if done:
+            break
     before = ctx.counters()
 
     # Device time of the K frames, from one HIP event pair on the launch
@@ -205,11 +233,12 @@ def main():
     # on MI355X — they stop the next launch's waves from overlapping the
     # previous one's tail — see scripts/host_overhead.py): average = bracket / K.
     # Tiled: the bracket is rank 0's stream (its shard, the gather, the de-interleave).
+    timed = timed_launches(step, stream, args.steps)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    launch_ms = timed_launches(step, stream, args.steps) / args.steps
+    launch_ms = timed() / args.steps
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -240,8 +269,9 @@ def main():
                 for _ in range(max(2, args.warmup)):
                     f1()
                 torch.cuda.synchronize()
+                timed1 = timed_launches(f1, stream, args.steps)
                 t1 = time.perf_counter()
-                timed_launches(f1, stream, args.steps)
+                timed1()
                 single_ms = (time.perf_counter() - t1) * 1e3 / args.steps
                 extra["single_gpu_ms_per_step"] = single_ms
                 extra["speedup_vs_1gpu"] = single_ms / (elapsed * 1e3 / args.steps)
@@ -264,6 +294,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_frames_run": warm_run,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
             "scaling": "strong" if tiled else "weak",
@@ -295,7 +326,7 @@ def main():
                 cold = []
                 for _ in range(3):
                     ctx.upload(scene)
-                    cold.append(timed_launches(step, stream, 1))
+                    cold.append(timed_launches(step, stream, 1)())
                 line["cold_kernel_ms"] = float(np.median(cold))
             # a drop-in Camera::render: synchronous rt_render into host memory,
             # PCIe copy included, into a canvas kept across frames (median of
