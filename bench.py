@@ -319,6 +319,10 @@ def main():
             line["roofline"]["kernel"] = "rank 0's shard launch (median of 5 instrumented frames)"
         line.update(extra)
         line["first_frame_ms"] = first_frame_ms
+        try:  # per-scene build time inside first_frame_ms (hipRTC, or a load from RTC_JIT_CACHE)
+            line["jit_build_ms"] = ctx.jit_status()["compile_ms"]
+        except Exception:  # noqa: BLE001  (group contexts may not report it)
+            pass
         if not tiled and world == 1:
             if ctx.scene.has_secondary() and args.depth > 0:
                 # cold launch: the first frame after an upload runs tiles in

@@ -300,7 +300,9 @@ int rt_debug_normal(rt_context* ctx, uint32_t shape, const double* points, uint6
  * at least 64K pixels (the default; env RTC_JIT=0|1 overrides at context
  * creation).  rt_jit_status: whether the last launch ran a per-scene kernel,
  * the compile milliseconds spent by this context, and the last build error
- * (a failed build keeps the generic kernel for that world). */
+ * (a failed build keeps the generic kernel for that world).  Builds are
+ * also cached on disk across processes: env RTC_JIT_CACHE = a directory, or
+ * 0 for none (default $XDG_CACHE_HOME/rtc_jit, else ~/.cache/rtc_jit). */
 int rt_context_set_jit(rt_context* ctx, int mode);
 int rt_jit_status(rt_context* ctx, int* used_last_launch, double* compile_ms, char* log, size_t log_len);
 

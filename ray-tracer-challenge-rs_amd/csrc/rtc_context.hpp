@@ -112,7 +112,8 @@ struct rt_context {
     hipFunction_t jit_fn[4] = {};
     int jit_mode = 2;
     bool jit_failed = false, jit_used = false;
-    double jit_compile_ms = 0;
+    double jit_compile_ms = 0;  // compile (or disk-cache load) time of this context's per-scene builds
+    int jit_cache_hits = 0;     // builds loaded from the on-disk cache
     std::string jit_log;
     // rt_render: counters before/after and the error flag come back pinned,
     // on the stream, so a frame needs one host sync

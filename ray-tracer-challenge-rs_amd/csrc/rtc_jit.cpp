@@ -12,10 +12,15 @@
 // kernel (tests/test_gpu_jit.py); only the f32 frame kernels are built this
 // way (the f64 parity path, rt_color_at and small frames keep the generic
 // kernels).  Builds are cached per process by table content and device, and
-// a failed build falls back to the generic kernel for that world.
+// on disk by everything the compiler sees (source, scene header, options,
+// hipRTC version), so a later process loads the code object instead of
+// compiling it (RTC_JIT_CACHE: a directory, or 0 for none; default
+// $XDG_CACHE_HOME/rtc_jit or ~/.cache/rtc_jit).  A failed build falls back to
+// the generic kernel for that world.
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <cerrno>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -25,6 +30,9 @@
 #include <mutex>
 #include <string>
 #include <vector>
+
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include "rtc_context.hpp"
 #include "rtc_jit_sources.inc"  // kSrcKernels, kSrcInternal, kSrcRtcH (tools/embed_sources.py)
@@ -77,7 +85,68 @@ struct CodeObject {
     std::vector<char> code;
     std::string lowered;
     double compile_ms = 0;
+    bool from_disk = false;
 };
+
+// ------------------------------------------------------- on-disk code cache
+// One file per build: "RTCJIT1\n" <lowered name> "\n" <code object>, named
+// by a 64-bit FNV-1a of every input of the compile.  Written to a temporary
+// name and renamed, so concurrent processes never read a partial file.
+constexpr char kCacheMagic[] = "RTCJIT1\n";
+
+std::string cache_dir() {
+    const char* e = std::getenv("RTC_JIT_CACHE");
+    if (e) return (!*e || !std::strcmp(e, "0")) ? std::string() : std::string(e);
+    if (const char* x = std::getenv("XDG_CACHE_HOME"); x && *x) return std::string(x) + "/rtc_jit";
+    if (const char* h = std::getenv("HOME"); h && *h) return std::string(h) + "/.cache/rtc_jit";
+    return std::string();
+}
+
+bool make_dirs(const std::string& d) {
+    for (size_t p = 1; p <= d.size(); ++p) {
+        if (p < d.size() && d[p] != '/') continue;
+        const std::string part = d.substr(0, p);
+        if (::mkdir(part.c_str(), 0755) != 0 && errno != EEXIST) return false;
+    }
+    return true;
+}
+
+std::string cache_path(const std::string& dir, uint64_t key) {
+    char buf[32];
+    std::snprintf(buf, sizeof buf, "/%016llx.co", (unsigned long long)key);
+    return dir + buf;
+}
+
+bool cache_load(const std::string& path, CodeObject& out) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    std::vector<char> all;
+    char buf[1 << 16];
+    for (size_t n; (n = std::fread(buf, 1, sizeof buf, f)) > 0;) all.insert(all.end(), buf, buf + n);
+    std::fclose(f);
+    const size_t m = sizeof kCacheMagic - 1;
+    if (all.size() < m || std::memcmp(all.data(), kCacheMagic, m)) return false;
+    size_t nl = m;
+    while (nl < all.size() && all[nl] != '\n') ++nl;
+    if (nl + 1 >= all.size() || nl == m) return false;
+    out.lowered.assign(all.data() + m, nl - m);
+    out.code.assign(all.begin() + (ptrdiff_t)(nl + 1), all.end());
+    out.from_disk = true;
+    return true;
+}
+
+void cache_store(const std::string& dir, const std::string& path, const CodeObject& co) {
+    if (!make_dirs(dir)) return;
+    const std::string tmp = path + ".tmp" + std::to_string((long long)::getpid());
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) return;
+    bool ok = std::fwrite(kCacheMagic, 1, sizeof kCacheMagic - 1, f) == sizeof kCacheMagic - 1;
+    ok = ok && std::fwrite(co.lowered.data(), 1, co.lowered.size(), f) == co.lowered.size();
+    ok = ok && std::fputc('\n', f) != EOF;
+    ok = ok && std::fwrite(co.code.data(), 1, co.code.size(), f) == co.code.size();
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
+}
 
 // Process-wide caches: code objects by (table, kernel); loaded functions by
 // (code object, device).
@@ -132,6 +201,25 @@ int compile(const std::string& scene, const char* name, CodeObject& out, std::st
         }
     }
     for (const std::string& x : extra) opts.push_back(x.c_str());
+    // the disk cache key: every input of the compile
+    int vmaj = 0, vmin = 0;
+    hiprtcVersion(&vmaj, &vmin);
+    uint64_t key = fnv(main_src.data(), main_src.size());
+    for (const char* h : headers) key = fnv(h, std::strlen(h) + 1, key);
+    for (const char* o : opts) key = fnv(o, std::strlen(o) + 1, key);
+    key = fnv(name, std::strlen(name) + 1, key);
+    const int ver[2] = {vmaj, vmin};
+    key = fnv(ver, sizeof ver, key);
+    const std::string dir = cache_dir();
+    const std::string path = dir.empty() ? std::string() : cache_path(dir, key);
+    if (!path.empty()) {
+        const auto c0 = std::chrono::steady_clock::now();
+        if (cache_load(path, out)) {
+            hiprtcDestroyProgram(&prog);
+            out.compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
+            return RT_OK;
+        }
+    }
     const auto t0 = std::chrono::steady_clock::now();
     const hiprtcResult r = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     out.compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -151,6 +239,7 @@ int compile(const std::string& scene, const char* name, CodeObject& out, std::st
         out.code.resize(cs);
         hiprtcGetCode(prog, out.code.data());
         if (out.lowered.empty() || cs == 0) rc = set_error(RT_ERR_HIP, "hipRTC produced no kernel");
+        else if (!path.empty()) cache_store(dir, path, out);
         if (const char* dir = std::getenv("RTC_JIT_DUMP")) {  // diagnostics: scene header + code object
             const std::string base = std::string(dir) + "/" + std::to_string(fnv(scene.data(), scene.size())) + "_" +
                                      (std::strstr(name, "pool") ? "pool" : "direct");
@@ -198,6 +287,7 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
             return RT_OK;
         }
         ctx->jit_compile_ms += built->compile_ms;
+        if (built->from_disk) ++ctx->jit_cache_hits;
         std::lock_guard<std::mutex> lk(g_mu);
         co = g_code.emplace(std::make_pair(key, variant), built).first->second;
     }

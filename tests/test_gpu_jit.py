@@ -82,3 +82,47 @@ def test_default_threshold_uses_the_per_scene_kernel_for_large_frames(gpu_ctx, r
     assert gpu_ctx.jit_status()["used"]
     gpu_ctx.render(rtc.camera_resize(scene.camera, 640, 480), 6, precision="f64")
     assert not gpu_ctx.jit_status()["used"]  # the f64 parity path is never rebuilt
+
+
+_CACHE_PROBE = r"""
+import hashlib, json, os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "ray-tracer-challenge-rs_amd"))
+import rtc_amd
+from rtc_amd import scene_io
+scene = scene_io.load(os.path.join(sys.argv[1], "tests", "golden", "scenes", "three_sphere_scene.json"))
+cam = rtc_amd.camera_resize(scene.camera, 320, 200)
+with rtc_amd.Context(0) as ctx:
+    ctx.upload(scene)
+    ctx.set_jit(1)
+    img, st = ctx.render(cam, 5, precision="f32")
+    js = ctx.jit_status()
+print(json.dumps({"used": js["used"], "ms": js["compile_ms"], "rays": st["rays"],
+                  "sha": hashlib.sha256(img.tobytes()).hexdigest()}))
+"""
+
+
+def test_per_scene_build_disk_cache(tmp_path):
+    """A second process loads the first one's per-scene build from the
+    RTC_JIT_CACHE directory instead of compiling it: same frame, bit for bit,
+    and no compile time."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RTC_JIT_CACHE=str(tmp_path / "cache"))
+
+    def run():
+        out = subprocess.run([sys.executable, "-c", _CACHE_PROBE, root], env=env, capture_output=True, text=True,
+                             timeout=100)
+        assert out.returncode == 0, out.stderr[-2000:]
+        return json.loads(out.stdout.strip().splitlines()[-1])
+
+    first = run()
+    files = sorted(p.name for p in (tmp_path / "cache").iterdir())
+    second = run()
+    assert first["used"] and second["used"]
+    assert len(files) == 1 and files[0].endswith(".co"), files
+    assert first["sha"] == second["sha"] and first["rays"] == second["rays"]
+    # a hipRTC build of the direct kernel takes ~300 ms; a cache load a few ms
+    assert first["ms"] > 50 and second["ms"] < 0.25 * first["ms"], (first["ms"], second["ms"])
