@@ -275,6 +275,10 @@ def main():
                 single_ms = (time.perf_counter() - t1) * 1e3 / args.steps
                 extra["single_gpu_ms_per_step"] = single_ms
                 extra["speedup_vs_1gpu"] = single_ms / (elapsed * 1e3 / args.steps)
+                # the same workload's throughput on one GPU, in the line's unit: the
+                # denominator for this line's scaling (the default N=1 line is
+                # configs[1], three_sphere at 1080p, a different workload)
+                extra["single_gpu_value"] = total_rays / args.steps / (single_ms * 1e-3) / 1e6
         if world > 1:
             dist.barrier()
     else:
