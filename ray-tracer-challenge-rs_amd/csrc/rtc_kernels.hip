@@ -178,13 +178,37 @@ __device__ inline V3<R> along(V3<R> p, V3<R> d, R t) {
     return {Real<R>::madd(d.x, t, p.x), Real<R>::madd(d.y, t, p.y), Real<R>::madd(d.z, t, p.z)};
 }
 
+// Transform terms of the f32 path.  In a per-scene build (RTC_JIT) a shape
+// record's matrix entries are compile-time constants, and most reference
+// shapes are scaled and translated only: a 3x3 part with six exact zeros.
+// A zero entry's term m * x is a signed zero, and adding a signed zero to a
+// nonzero partial sum leaves it unchanged, so the term is dropped: 12 of the
+// 21 transform operations of such a shape (the ray's components are finite on
+// every lane whose result is used).  Only the sign of an exactly-zero
+// coordinate can differ, and no later operation depends on it (divisions by
+// a ray component are guarded by |d| >= EPSILON); the per-scene frames stay
+// bit-identical to the generic kernel's (tests/test_gpu_jit.py).  The
+// generic kernels read the records at run time and keep every term.
+__device__ inline float kfma(float m, float x, float acc) {
+#ifdef RTC_JIT
+    if (__builtin_constant_p(m) && m == 0.0f) return acc;
+#endif
+    return __builtin_fmaf(m, x, acc);
+}
+__device__ inline float kmul(float m, float x) {
+#ifdef RTC_JIT
+    if (__builtin_constant_p(m) && m == 0.0f) return 0.0f;
+#endif
+    return m * x;
+}
+
 // matrix.rs:332-346 (w = 1), left fold from 0.0
 template <typename R>
 __device__ inline V3<R> xform_point(const R* m, V3<R> p) {
     if constexpr (sizeof(R) == 4) {
-        return {__builtin_fmaf(m[2], p.z, __builtin_fmaf(m[1], p.y, __builtin_fmaf(m[0], p.x, m[3]))),
-                __builtin_fmaf(m[6], p.z, __builtin_fmaf(m[5], p.y, __builtin_fmaf(m[4], p.x, m[7]))),
-                __builtin_fmaf(m[10], p.z, __builtin_fmaf(m[9], p.y, __builtin_fmaf(m[8], p.x, m[11])))};
+        return {kfma(m[2], p.z, kfma(m[1], p.y, kfma(m[0], p.x, m[3]))),
+                kfma(m[6], p.z, kfma(m[5], p.y, kfma(m[4], p.x, m[7]))),
+                kfma(m[10], p.z, kfma(m[9], p.y, kfma(m[8], p.x, m[11])))};
     } else {
         return {((((R)0 + m[0] * p.x) + m[1] * p.y) + m[2] * p.z) + m[3],
                 ((((R)0 + m[4] * p.x) + m[5] * p.y) + m[6] * p.z) + m[7],
@@ -195,9 +219,9 @@ __device__ inline V3<R> xform_point(const R* m, V3<R> p) {
 template <typename R>
 __device__ inline V3<R> xform_vector(const R* m, V3<R> v) {
     if constexpr (sizeof(R) == 4) {
-        return {__builtin_fmaf(m[2], v.z, __builtin_fmaf(m[1], v.y, m[0] * v.x)),
-                __builtin_fmaf(m[6], v.z, __builtin_fmaf(m[5], v.y, m[4] * v.x)),
-                __builtin_fmaf(m[10], v.z, __builtin_fmaf(m[9], v.y, m[8] * v.x))};
+        return {kfma(m[2], v.z, kfma(m[1], v.y, kmul(m[0], v.x))),
+                kfma(m[6], v.z, kfma(m[5], v.y, kmul(m[4], v.x))),
+                kfma(m[10], v.z, kfma(m[9], v.y, kmul(m[8], v.x)))};
     } else {
         return {(((R)0 + m[0] * v.x) + m[1] * v.y) + m[2] * v.z + m[3] * (R)0,
                 (((R)0 + m[4] * v.x) + m[5] * v.y) + m[6] * v.z + m[7] * (R)0,
