@@ -232,9 +232,9 @@ __device__ inline V3<R> xform_vector(const R* m, V3<R> v) {
 template <typename R>
 __device__ inline V3<R> xform_normal(const R* m, V3<R> n) {
     if constexpr (sizeof(R) == 4) {
-        return {__builtin_fmaf(m[8], n.z, __builtin_fmaf(m[4], n.y, m[0] * n.x)),
-                __builtin_fmaf(m[9], n.z, __builtin_fmaf(m[5], n.y, m[1] * n.x)),
-                __builtin_fmaf(m[10], n.z, __builtin_fmaf(m[6], n.y, m[2] * n.x))};
+        return {kfma(m[8], n.z, kfma(m[4], n.y, kmul(m[0], n.x))),
+                kfma(m[9], n.z, kfma(m[5], n.y, kmul(m[1], n.x))),
+                kfma(m[10], n.z, kfma(m[6], n.y, kmul(m[2], n.x)))};
     } else {
         return {(((R)0 + m[0] * n.x) + m[4] * n.y) + m[8] * n.z,
                 (((R)0 + m[1] * n.x) + m[5] * n.y) + m[9] * n.z,
@@ -755,6 +755,51 @@ __device__ inline V3<R> normal_at(const ShapeRec<R>& s, int kind, V3<R> p) {
     return normalized(xform_normal(s.inv, local_normal(s, kind, xform_point(s.inv, p))));
 }
 
+#ifdef RTC_JIT
+// Per-scene build of a small world: the hit's normal from the constant
+// record of its slot.  Each slot present among a wave's hits runs its own
+// case (an exec-masked branch per slot), where the kind is known and the
+// record's matrix is made of immediates: a plane's world normal before
+// normalisation is a constant, a scaled sphere's transforms lose their zero
+// terms (kfma).  The generic path reads the record from LDS and runs every
+// kind's transforms.  The unnormalised normal passes an empty asm so the
+// hardware rsq runs as in the generic kernel (the compiler would fold it for
+// a constant with a correctly rounded 1/sqrt): frames stay bit-identical.
+#ifndef RTC_JIT_NORMAL_MAX
+#define RTC_JIT_NORMAL_MAX 8
+#endif
+template <int I>
+constexpr int jit_kind_of() {
+    int k = 0;
+    while (jit::kBegin[k + 1] <= I) ++k;
+    return k;
+}
+template <int I, int E>
+__device__ inline void jit_normal_each(int slot, V3<float> p, V3<float>& w) {
+    if constexpr (I < E) {
+        if (slot == I) {
+            const ShapeRec<float>& s = jit::kShapes[I];
+            w = xform_normal(s.inv, local_normal(s, jit_kind_of<I>(), xform_point(s.inv, p)));
+        }
+        jit_normal_each<I + 1, E>(slot, p, w);
+    }
+}
+#endif
+
+template <typename R>
+__device__ inline V3<R> hit_normal(const ShapeRec<R>& s, int slot, int kind, V3<R> p) {
+#ifdef RTC_JIT
+    if constexpr (sizeof(R) == 4 && jit::kBegin[kNumKinds] <= RTC_JIT_NORMAL_MAX) {
+        V3<float> w = {0.0f, 0.0f, 0.0f};
+        jit_normal_each<0, jit::kBegin[kNumKinds]>(slot, p, w);
+        asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(w.z));
+        return normalized(w);
+    }
+#endif
+    (void)slot;
+    return normal_at(s, kind, p);
+}
+
 // Pattern::color_at_shape (pattern.rs:10-14) and the five color_at bodies.
 template <typename R>
 __device__ inline V3<R> pattern_color(const DevScene<R>& sc, int pid, const ShapeRec<R>& s, V3<R> p) {
@@ -855,7 +900,7 @@ __device__ inline const MaterialRec<R>& prepare_hit(const DevScene<R>& sc, V3<R>
                                                      Prepared<R>& q, bool& patterned) {
     const ShapeRec<R>& s = sc.lshapes[h.slot];
     q.p = along(o, d, h.t);
-    q.n = normal_at(s, h.kind, q.p);
+    q.n = hit_normal(s, h.slot, h.kind, q.p);
     q.eye = vneg(d);
     if (dot(q.n, q.eye) < (R)0) q.n = vneg(q.n);
     const MaterialRec<R>& m = sc.lmats[s.material];
