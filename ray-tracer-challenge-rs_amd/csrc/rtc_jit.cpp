@@ -86,13 +86,17 @@ struct CodeObject {
     std::string lowered;
     double compile_ms = 0;
     bool from_disk = false;
+    uint64_t key = 0;  // the disk cache key (every input of the compile)
 };
 
 // ------------------------------------------------------- on-disk code cache
-// One file per build: "RTCJIT1\n" <lowered name> "\n" <code object>, named
-// by a 64-bit FNV-1a of every input of the compile.  Written to a temporary
-// name and renamed, so concurrent processes never read a partial file.
-constexpr char kCacheMagic[] = "RTCJIT1\n";
+// One file per build: "RTCJIT2\n" <lowered name> "\n" <code bytes> " "
+// <FNV-1a of the code, hex> "\n" <code object>, named by a 64-bit FNV-1a of
+// every input of the compile.  Written to a temporary name and renamed, so
+// concurrent processes never read a partial file; a file whose length or
+// checksum does not match is ignored and rebuilt (a damaged code object
+// handed to hipModuleLoadData can abort the process instead of failing).
+constexpr char kCacheMagic[] = "RTCJIT2\n";
 
 std::string cache_dir() {
     const char* e = std::getenv("RTC_JIT_CACHE");
@@ -129,8 +133,15 @@ bool cache_load(const std::string& path, CodeObject& out) {
     size_t nl = m;
     while (nl < all.size() && all[nl] != '\n') ++nl;
     if (nl + 1 >= all.size() || nl == m) return false;
+    size_t nl2 = nl + 1;
+    while (nl2 < all.size() && all[nl2] != '\n') ++nl2;
+    if (nl2 >= all.size()) return false;
+    unsigned long long len = 0, sum = 0;
+    const std::string meta(all.data() + nl + 1, nl2 - nl - 1);
+    if (std::sscanf(meta.c_str(), "%llu %llx", &len, &sum) != 2) return false;
+    if (len == 0 || all.size() - (nl2 + 1) != len || fnv(all.data() + nl2 + 1, len) != sum) return false;
     out.lowered.assign(all.data() + m, nl - m);
-    out.code.assign(all.begin() + (ptrdiff_t)(nl + 1), all.end());
+    out.code.assign(all.begin() + (ptrdiff_t)(nl2 + 1), all.end());
     out.from_disk = true;
     return true;
 }
@@ -142,7 +153,8 @@ void cache_store(const std::string& dir, const std::string& path, const CodeObje
     if (!f) return;
     bool ok = std::fwrite(kCacheMagic, 1, sizeof kCacheMagic - 1, f) == sizeof kCacheMagic - 1;
     ok = ok && std::fwrite(co.lowered.data(), 1, co.lowered.size(), f) == co.lowered.size();
-    ok = ok && std::fputc('\n', f) != EOF;
+    ok = ok && std::fprintf(f, "\n%llu %llx\n", (unsigned long long)co.code.size(),
+                            (unsigned long long)fnv(co.code.data(), co.code.size())) > 0;
     ok = ok && std::fwrite(co.code.data(), 1, co.code.size(), f) == co.code.size();
     ok = (std::fclose(f) == 0) && ok;
     if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
@@ -154,7 +166,7 @@ std::mutex g_mu;
 std::map<std::pair<uint64_t, int>, std::shared_ptr<CodeObject>> g_code;
 std::map<std::pair<uint64_t, int>, std::pair<hipModule_t, hipFunction_t>> g_fn;
 
-int compile(const std::string& scene, const char* name, CodeObject& out, std::string& log) {
+int compile(const std::string& scene, const char* name, CodeObject& out, std::string& log, bool use_cache = true) {
     const std::string main_src = std::string("#define RTC_JIT 1\n#include \"rtc_jit_scene.hpp\"\n") + kSrcKernels;
     const char* headers[] = {scene.c_str(), kSrcInternal, kSrcRtcH};
     const char* names[] = {"rtc_jit_scene.hpp", "rtc_internal.hpp", "../../include/rtc.h"};
@@ -210,8 +222,9 @@ int compile(const std::string& scene, const char* name, CodeObject& out, std::st
     key = fnv(name, std::strlen(name) + 1, key);
     const int ver[2] = {vmaj, vmin};
     key = fnv(ver, sizeof ver, key);
+    out.key = key;
     const std::string dir = cache_dir();
-    const std::string path = dir.empty() ? std::string() : cache_path(dir, key);
+    const std::string path = dir.empty() || !use_cache ? std::string() : cache_path(dir, key);
     if (!path.empty()) {
         const auto c0 = std::chrono::steady_clock::now();
         if (cache_load(path, out)) {

@@ -126,3 +126,11 @@ def test_per_scene_build_disk_cache(tmp_path):
     assert first["sha"] == second["sha"] and first["rays"] == second["rays"]
     # a hipRTC build of the direct kernel takes ~300 ms; a cache load a few ms
     assert first["ms"] > 50 and second["ms"] < 0.25 * first["ms"], (first["ms"], second["ms"])
+    # a damaged file (truncated code object) is rebuilt and rewritten, not trusted
+    f = tmp_path / "cache" / files[0]
+    size = f.stat().st_size
+    with open(f, "r+b") as fh:
+        fh.truncate(size // 2)
+    third = run()
+    assert third["used"] and third["sha"] == first["sha"], third
+    assert f.stat().st_size == size
