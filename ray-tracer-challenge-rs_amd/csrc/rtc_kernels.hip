@@ -472,8 +472,11 @@ __device__ inline bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) 
 // branch on the record and its loads issue together; cylinders, cones and
 // triangles keep a wave-uniform branch on r^2 < 0 (open cylinders and cones
 // are unbounded, their test would be wasted VALU).
+// dd = dot(d, d), formed once per ray by the caller: in the per-scene build
+// the ray fence between unrolled shapes would otherwise recompute it for
+// every shape.
 template <typename R, int K>
-__device__ inline bool wave_may_hit(const ShapeRec<R>& s, V3<R> o, V3<R> d) {
+__device__ inline bool wave_may_hit(const ShapeRec<R>& s, V3<R> o, V3<R> d, R dd) {
     if constexpr (K == RT_SHAPE_PLANE) return true;
     const R r2 = s.bound[3];  // radius^2
     if constexpr (K != RT_SHAPE_SPHERE && K != RT_SHAPE_CUBE)
@@ -489,7 +492,7 @@ __device__ inline bool wave_may_hit(const ShapeRec<R>& s, V3<R> o, V3<R> d) {
     // comparison, combined as SGPR masks (a ballot of the combined bool makes
     // the compiler materialise it in a VGPR and compare it again: 2 VALU)
     const unsigned long long front = __builtin_amdgcn_ballot_w64(tc >= (R)0) | __builtin_amdgcn_ballot_w64(oo <= r2);
-    return (front & __builtin_amdgcn_ballot_w64(Real<R>::madd(oo, kKeep, -r2) * dot(d, d) <= tc * tc)) != 0;
+    return (front & __builtin_amdgcn_ballot_w64(Real<R>::madd(oo, kKeep, -r2) * dd <= tc * tc)) != 0;
 }
 
 // Per-scene build only: the ray's registers pass through an empty asm at the
@@ -567,9 +570,10 @@ struct Nearest {
 template <typename R>
 __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
     Nearest<R> best;
+    const R dd = dot(d, d);
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
         jit_fence(o, d, slot);
-        if (!wave_may_hit<R, K>(s, o, d)) return;
+        if (!wave_may_hit<R, K>(s, o, d, dd)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
         const int w = s.world_index;
@@ -606,10 +610,11 @@ struct Blocker {
 template <typename R>
 __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) {
     Blocker<R> b;
+    const R dd = dot(d, d);
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
         if (!s.casts_shadow) return;  // wave-uniform
         jit_fence(o, d, slot);
-        if (!wave_may_hit<R, K>(s, o, d)) return;
+        if (!wave_may_hit<R, K>(s, o, d, dd)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
         entries<R, K>(s, lo, ld, [&](R t, bool v) { b.offer(t, v, dist); });
