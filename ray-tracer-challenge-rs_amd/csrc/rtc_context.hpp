@@ -90,6 +90,11 @@ struct rt_context {
     uint64_t order_geometry = 0;  // order_sig without the camera
     bool order_valid = false;
     bool order_built = false;     // d_tile_order holds an order for order_geometry
+    // First launch of a frame geometry (no recorded costs): tiles handed out
+    // centre-out instead of in raster order (RTC_COLD_ORDER=center|raster).
+    bool cold_center = true;
+    uint32_t* d_cold_order = nullptr;  // centre-out order + item count, for cold_w x cold_h
+    uint32_t cold_w = 0, cold_h = 0;
     // Tiles costing more than split_factor x the mean workgroup load are
     // handed out in parts (order_tiles); RTC_SPLIT=0 never splits.
     double split_factor = 1.5;

@@ -454,6 +454,32 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
     if (ctx->order_built) {  // built from this frame's costs, or from the previous camera's frame
         P.tile_order = ctx->d_tile_order;
         P.item_count = n_items;
+    } else if (ctx->cold_center && P.shard_count == 1) {
+        // No costs yet: tiles nearest the image centre first.  The order
+        // depends on the canvas only, so it is built and uploaded once per
+        // canvas size into its own buffer (order_tiles reuses d_tile_order).
+        if (!ctx->d_cold_order || ctx->cold_w != P.width || ctx->cold_h != P.height) {
+            const uint32_t n = P.n_tiles, tx = P.tiles_x;
+            std::vector<std::pair<uint64_t, uint32_t>> key(n);
+            const int64_t cx = (int64_t)P.width, cy = (int64_t)P.height;  // doubled centre
+            for (uint32_t t = 0; t < n; ++t) {
+                const int64_t x = 2 * (int64_t)((t % tx) * RT_TILE_W) + RT_TILE_W - cx;
+                const int64_t y = 2 * (int64_t)((t / tx) * RT_TILE_H) + RT_TILE_H - cy;
+                key[t] = {(uint64_t)(x * x + y * y), t};
+            }
+            std::sort(key.begin(), key.end());
+            std::vector<uint32_t> v(n + 1);
+            for (uint32_t i = 0; i < n; ++i) v[i] = key[i].second;
+            v[n] = n;
+            (void)hipFree(ctx->d_cold_order);
+            ctx->d_cold_order = nullptr;
+            RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_cold_order), v.size() * sizeof(uint32_t)));
+            RT_HIP(hipMemcpy(ctx->d_cold_order, v.data(), v.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+            ctx->cold_w = P.width;
+            ctx->cold_h = P.height;
+        }
+        P.tile_order = ctx->d_cold_order;
+        P.item_count = ctx->d_cold_order + P.n_tiles;
     }
     P.tile_cost = ctx->d_tile_cost;
     ctx->order_sig = h;
@@ -737,6 +763,7 @@ int create_device_context(int device_ordinal, rt_context** out) {
     if (const char* e = std::getenv("RTC_KIND_VARIANTS")) ctx->kind_variants = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_POOL_LDS_RAYS")) ctx->pool_lds_rays = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("RTC_TILE_ORDER")) ctx->tile_order = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("RTC_COLD_ORDER")) ctx->cold_center = !std::strcmp(e, "center");
     if (const char* e = std::getenv("RTC_SPLIT")) ctx->split_factor = std::atof(e);
     if (const char* e = std::getenv("RTC_ORDER_BUILDS")) ctx->order_max_builds = std::atoi(e);
     if (const char* e = std::getenv("RTC_DIRECT_GRID")) ctx->direct_grid = (uint32_t)std::atoi(e);
@@ -771,6 +798,7 @@ void destroy_device_context(rt_context* ctx) {
     (void)hipFree(ctx->d_spill);
     (void)hipFree(ctx->d_tile_cost);
     (void)hipFree(ctx->d_tile_order);
+    (void)hipFree(ctx->d_cold_order);
     if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
     if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
     if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
