@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <atomic>
 #include <cerrno>
 #include <chrono>
 #include <cstdio>
@@ -148,7 +149,8 @@ bool cache_load(const std::string& path, CodeObject& out) {
 
 void cache_store(const std::string& dir, const std::string& path, const CodeObject& co) {
     if (!make_dirs(dir)) return;
-    const std::string tmp = path + ".tmp" + std::to_string((long long)::getpid());
+    static std::atomic<unsigned> seq{0};  // contexts of one process may build the same key at once
+    const std::string tmp = path + ".tmp" + std::to_string((long long)::getpid()) + "." + std::to_string(seq++);
     FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f) return;
     bool ok = std::fwrite(kCacheMagic, 1, sizeof kCacheMagic - 1, f) == sizeof kCacheMagic - 1;
