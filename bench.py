@@ -238,10 +238,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    launch_ms = timed() / args.steps
+    launch_ms = timed() / args.steps  # ends with torch.cuda.synchronize()
+    # each rank's clock stops at its own synchronize; the closing barrier is
+    # outside it (a gloo barrier costs ~0.1-1 ms against a 7 ms 20-frame tiled
+    # region) and the max over ranks is taken below (rdist.job_totals).  In
+    # tiled mode rank 0's stream holds the gather, which waits for every shard.
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     after = ctx.counters()
 
     rays = after["rays"] - before["rays"]
