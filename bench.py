@@ -113,6 +113,31 @@ def cpu_baseline(scene, cam, depth, budget_s):
                       f"f64 C++ restatement of Camera::render_parallel, {dt:.1f}s on {threads} threads"}
 
 
+def cpu_serial_configs0(budget_s):
+    """BASELINE configs[0]: three_sphere_scene at 320x240 in serial CPU mode,
+    i.e. the f64 oracle's restatement of Camera::render (camera.rs:79-95) on
+    one thread, whole frames until `budget_s` elapses (at least 3)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    import rtc_amd
+    from rtc_amd import scene_io
+    scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", "three_sphere_scene.json"))
+    cam = rtc_amd.camera_resize(scene.camera, 320, 240)
+    times, rays = [], 0
+    t0 = time.perf_counter()
+    while len(times) < 3 or time.perf_counter() - t0 < budget_s:
+        t = time.perf_counter()
+        _, st = pyoracle.render(scene, cam, 6, threads=1)
+        times.append(time.perf_counter() - t)
+        rays += st["rays"]
+    import statistics
+    ms = statistics.median(times) * 1e3
+    return {"config": "scenes/three_sphere_scene.yaml at 320x240, serial CPU mode (BASELINE configs[0])",
+            "ms_per_frame": ms, "value": rays / sum(times) / 1e6, "unit": "Mray/s", "cores": 1,
+            "kind": "port", "rays_per_frame": st["rays"],
+            "sample": f"{len(times)} frames, f64 C++ restatement of Camera::render on 1 thread, median ms/frame"}
+
+
 def load_traffic(workload: str):
     """HBM bytes per launch from the committed rocprofv3 --pmc pass (profiles/traffic.json)."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
@@ -353,6 +378,7 @@ def main():
             line["host_frame_ms"] = float(np.median(lat))
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(scene, cam, args.depth, args.cpu_seconds)
+            line["cpu_baseline"]["configs0_serial"] = cpu_serial_configs0(min(3.0, args.cpu_seconds / 4))
         print(json.dumps(line), flush=True)
     ctx.close()
     if world > 1:

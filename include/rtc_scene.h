@@ -9,7 +9,8 @@
  *       scene_loader.rs:255-266, camera.rs:25-49/124-127,
  *       transformations.rs:75-87                      -> rt_camera_make
  *   Matrix<4>::inverse  primitives/matrix.rs:247-258  -> rt_matrix_inverse
- *   Canvas::to_png_file / to_ppm  canvas.rs:75-137    -> rt_image_write
+ *   Canvas::to_png_file / to_ppm_file  canvas.rs:75-137 -> rt_image_write
+ *   Color::clamped + u8 cast  canvas.rs:81, 117-123   -> rt_canvas_quantize
  * All arithmetic is f64 and follows the reference's operation order, so the
  * tables are bit-identical to what the reference holds after loading.
  * Pure host code: none of these functions needs a GPU.
@@ -65,12 +66,28 @@ int rt_camera_set_transform(rt_camera_desc* camera, const double transform[16]);
 /* Matrix<4>::inverse, row-major 16 doubles. */
 int rt_matrix_inverse(const double m[16], double out[16]);
 
-/* Canvas::to_png_file / to_ppm (canvas.rs:75-137) for an 8-bit frame
+/* Canvas::to_png_file / to_ppm_file (canvas.rs:75-137) for an 8-bit frame
  * (rt_render with RT_OUT_U8, row-major RGB, y = 0 at the top): a path ending
  * in ".png" (any case) gets an RGB8 PNG (filter None, best deflate, as the
- * reference writes), anything else a binary PPM (P6).  RT_ERR_IO on a write
- * failure.  Host only. */
+ * reference writes), anything else the reference's P3 text byte for byte
+ * (canvas.rs:75-97: 5 pixels per line across row boundaries, channels
+ * right-aligned to width 3, no trailing newline).  The parent directories
+ * are created first (canvas.rs:99-105).  RT_ERR_IO on a write failure.
+ * Host only. */
 int rt_image_write(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height);
+
+enum {
+    RT_IMAGE_AUTO = 0,        /* by extension, as rt_image_write */
+    RT_IMAGE_PNG = 1,         /* Canvas::to_png_file */
+    RT_IMAGE_PPM = 2,         /* Canvas::to_ppm_file: P3 text, the reference's bytes */
+    RT_IMAGE_PPM_BINARY = 3   /* P6 (not in the reference): the same pixels in 1/4 of the bytes */
+};
+int rt_image_write_format(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height, int format);
+
+/* The canvas's 8-bit quantization on the host (canvas.rs:81, 117-123):
+ * round(clamp(c, 0, 1) * 255), half away from zero, NaN -> 0, for f64
+ * canvases (the kernels quantize RT_OUT_U8 frames themselves). */
+int rt_canvas_quantize(const double* rgb, uint64_t n_channels, uint8_t* out);
 
 #ifdef __cplusplus
 }

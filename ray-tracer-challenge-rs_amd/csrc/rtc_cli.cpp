@@ -1,9 +1,10 @@
 // rtc_cli.cpp — command-line driver mirroring ray-tracer-cli/src/main.rs:11-31
 // and cli/cli_arguments.rs:4-13: `<SCENE> <OUT> [-r serial|parallel] [-q]`,
 // timing of the render call only (main.rs:17-24), then the PNG save
-// (main.rs:26, canvas.rs:114-137; OUT ending in anything but .png gets a
-// binary PPM).  The reference's rendering modes pick Camera::render or
-// render_parallel; here every mode renders on the GPU (the library owns the
+// (main.rs:26, canvas.rs:114-137; OUT ending in anything but .png gets the
+// reference's P3 text, canvas.rs:75-97, or a binary P6 with --ppm-binary).
+// The reference's rendering modes pick Camera::render or render_parallel;
+// here every mode renders on the GPU (the library owns the
 // parallelism), so `-r serial|parallel|gpu` are accepted and equivalent.
 // Extra flags: --width/--height (same as editing the YAML camera size),
 // --depth (World::MAX_REFLECTION_ITERATIONS = 6 by default), --precision
@@ -23,7 +24,7 @@
 static int usage() {
     std::fprintf(stderr,
                  "usage: rtc <SCENE.yaml> <OUT.png|OUT.ppm> [-r serial|parallel|gpu] [-q] [--width W] [--height H]\n"
-                 "           [--depth D] [--precision f32|f64] [--device N] [--gpus N]\n");
+                 "           [--depth D] [--precision f32|f64] [--device N] [--gpus N] [--ppm-binary]\n");
     return 2;
 }
 
@@ -31,13 +32,14 @@ int main(int argc, char** argv) {
     if (argc < 3) return usage();
     const char* scene_path = argv[1];
     const char* out_path = argv[2];
-    bool quiet = false;
+    bool quiet = false, ppm_binary = false;
     uint32_t width = 0, height = 0, depth = RT_DEFAULT_MAX_DEPTH, precision = RT_PRECISION_F32;
     int device = 0, gpus = 1;
     for (int i = 3; i < argc; ++i) {
         std::string a = argv[i];
         auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : nullptr; };
         if (a == "-q" || a == "--quiet") quiet = true;
+        else if (a == "--ppm-binary") ppm_binary = true;
         else if (a == "-r" || a == "--rendering-mode") {
             const char* v = next();
             if (!v || (std::strcmp(v, "serial") && std::strcmp(v, "parallel") && std::strcmp(v, "gpu"))) return usage();
@@ -93,7 +95,8 @@ int main(int argc, char** argv) {
                     (unsigned long long)st.primary, (unsigned long long)st.shadow, (unsigned long long)st.reflect,
                     (unsigned long long)st.refract, rays / (st.kernel_ms * 1e3));
     }
-    if (rt_image_write(out_path, img.data(), cam.width, cam.height) != RT_OK) {
+    if (rt_image_write_format(out_path, img.data(), cam.width, cam.height,
+                              ppm_binary ? RT_IMAGE_PPM_BINARY : RT_IMAGE_AUTO) != RT_OK) {
         std::fprintf(stderr, "error: %s\n", rt_last_error());
         return 1;
     }

@@ -168,6 +168,8 @@ def _load() -> C.CDLL:
         "rt_scene_view_get": (C.c_int, [C.c_void_p, P(SceneView)]),
         "rt_scene_free": (None, [C.c_void_p]),
         "rt_image_write": (C.c_int, [C.c_char_p, C.c_void_p, C.c_uint32, C.c_uint32]),
+        "rt_image_write_format": (C.c_int, [C.c_char_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_int]),
+        "rt_canvas_quantize": (C.c_int, [P(C.c_double), C.c_uint64, P(C.c_uint8)]),
         "rt_camera_make": (C.c_int, [C.c_uint32, C.c_uint32, C.c_double, P(C.c_double), P(C.c_double),
                                      P(C.c_double), P(CameraDesc)]),
         "rt_camera_resize": (C.c_int, [P(CameraDesc), C.c_uint32, C.c_uint32]),
@@ -204,7 +206,8 @@ EXPORTED_SYMBOLS = (
     "rt_shard_row_map", "rt_context_create_multi", "rt_comm_unique_id", "rt_context_create_rank", "rt_context_group",
     "rt_context_set_jit", "rt_jit_status",
     "rt_assemble_shards", "rt_scene_load_yaml", "rt_scene_load_yaml_text", "rt_scene_view_get", "rt_scene_free",
-    "rt_camera_make", "rt_camera_resize", "rt_matrix_inverse", "rt_image_write",
+    "rt_camera_make", "rt_camera_resize", "rt_matrix_inverse", "rt_image_write", "rt_image_write_format",
+    "rt_canvas_quantize",
 )
 
 
@@ -254,13 +257,27 @@ def camera_resize(cam: CameraDesc, width: int, height: int) -> CameraDesc:
     return c
 
 
-def write_image(path, image: np.ndarray) -> None:
-    """Canvas::to_png_file / to_ppm (canvas.rs:75-137) of an 8-bit (H, W, 3) frame
-    (render(..., out_format="u8")): PNG when `path` ends in .png, binary PPM otherwise."""
+IMAGE_FORMATS = {"auto": 0, "png": 1, "ppm": 2, "ppm-binary": 3}
+
+
+def write_image(path, image: np.ndarray, fmt: str = "auto") -> None:
+    """Canvas::to_png_file / to_ppm_file (canvas.rs:75-137) of an 8-bit (H, W, 3) frame
+    (render(..., out_format="u8")): PNG when `path` ends in .png, the reference's P3
+    text otherwise; fmt "ppm-binary" writes P6 instead (an opt-in, not the reference's)."""
     img = np.ascontiguousarray(image)
     if img.dtype != np.uint8 or img.ndim != 3 or img.shape[2] != 3:
         raise ValueError("write_image takes a uint8 array of shape (H, W, 3)")
-    _check(_lib.rt_image_write(os.fsencode(path), img.ctypes.data, img.shape[1], img.shape[0]))
+    _check(_lib.rt_image_write_format(os.fsencode(path), img.ctypes.data if img.size else None, img.shape[1],
+                                      img.shape[0], IMAGE_FORMATS[fmt]))
+
+
+def canvas_quantize(image: np.ndarray) -> np.ndarray:
+    """canvas.rs:81, 117-123 on the host: round(clamp(c, 0, 1) * 255) as u8 of an f64 canvas."""
+    src = np.ascontiguousarray(image, dtype=np.float64)
+    out = np.zeros(src.shape, dtype=np.uint8)
+    _check(_lib.rt_canvas_quantize(src.ctypes.data_as(C.POINTER(C.c_double)), src.size,
+                                   out.ctypes.data_as(C.POINTER(C.c_uint8))))
+    return out
 
 
 def shard_rows(height: int, shard_count: int) -> int:

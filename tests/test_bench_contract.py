@@ -45,6 +45,8 @@ def test_bench_line_contract():
     assert abs(rl["frac"] - rl["achieved"] / rl["peak"]) < 1e-12
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
+    s0 = cb["configs0_serial"]  # BASELINE configs[0]: Camera::render at 320x240, one thread
+    assert s0["cores"] == 1 and s0["ms_per_frame"] > 0 and s0["rays_per_frame"] == 2 * 320 * 240
 
 
 @pytest.mark.gpu

@@ -46,12 +46,17 @@ SCENE = """
 """
 
 
-def read_ppm(path):
+def read_ppm(path, magic=b"P3"):
+    """The CLI saves .ppm as the reference's P3 text (canvas.rs:75-97); P6 with --ppm-binary."""
     data = open(path, "rb").read()
     parts = data.split(b"\n", 3)
-    assert parts[0] == b"P6" and parts[2] == b"255"
+    assert parts[0] == magic and parts[2] == b"255"
     w, h = map(int, parts[1].split())
-    return np.frombuffer(parts[3], dtype=np.uint8).reshape(h, w, 3)
+    if magic == b"P6":
+        return np.frombuffer(parts[3], dtype=np.uint8).reshape(h, w, 3)
+    lines = parts[3].split(b"\n")
+    assert not data.endswith(b"\n") and all(len(x) == 15 * 4 - 1 for x in lines[:-1])
+    return np.array(parts[3].split(), dtype=np.int64).astype(np.uint8).reshape(h, w, 3)
 
 
 def test_cli_usage_and_missing_scene_fail_loudly(tmp_path):
@@ -94,3 +99,8 @@ def test_cli_png_equals_ppm(tmp_path):
         outs[ext] = out
     with PIL.open(outs["png"]) as im:
         assert np.array_equal(np.asarray(im.convert("RGB")), read_ppm(outs["ppm"]))
+    out = tmp_path / "out_p6.ppm"
+    r = subprocess.run([CLI, str(yaml), str(out), "--ppm-binary", "-q", "--width", "64", "--height", "48"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(read_ppm(out, b"P6"), read_ppm(outs["ppm"]))

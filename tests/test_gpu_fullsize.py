@@ -1,5 +1,9 @@
 """BASELINE configs at their own sizes, HIP path against the f64 oracle.
 
+  configs[0]  three_sphere_scene 320x240   against the oracle's SERIAL
+              Camera::render (camera.rs:79-95): f64 within 1e-9 with equal
+              counters, the u8 canvas, f32
+  configs[1]  three_sphere_scene 1920x1080 (tests/test_gpu_parity.py)
   configs[2]  reflect_refract   1920x1080  (f32 and f64)
   configs[3]  cover             3840x2160  (f32 and f64; + the 8-shard split)
   configs[4]  table             3840x2160  (f32 and f64)
@@ -39,6 +43,25 @@ def _oracle_frame(oracle, rtc, name):
         _ref_cache.clear()  # one 4K f64 frame (200 MB) at a time
         _ref_cache[name] = (scene, cam) + oracle.render(scene, cam, 6, threads=ORACLE_THREADS)
     return _ref_cache[name]
+
+
+def test_config0_against_serial_render(gpu_ctx, oracle, rtc):
+    scene = scene_fixture("three_sphere_scene")
+    cam = rtc.camera_resize(scene.camera, 320, 240)
+    ref, rst = oracle.render(scene, cam, 6, threads=1)  # Camera::render, serial
+    gpu_ctx.upload(scene)
+    img, st = gpu_ctx.render(cam, 6, precision="f64")
+    assert np.abs(img - ref).max() < ABS64
+    assert _counts(st) == _counts(rst) and st["rays"] == 2 * 320 * 240
+    # the u8 canvas the f64 kernel stores is the reference's quantization of its frame
+    # (canvas.rs:117-123), and within 1 LSB of the serial frame's (a 1e-9 difference
+    # can cross a rounding boundary)
+    u8, _ = gpu_ctx.render(cam, 6, precision="f64", out_format="u8")
+    assert np.array_equal(u8, oracle.quantize(img))
+    assert np.abs(u8.astype(np.int16) - oracle.quantize(ref).astype(np.int16)).max() <= 1
+    img32, st32 = gpu_ctx.render(cam, 5, precision="f32")  # BASELINE's "depth 5"
+    d = np.abs(oracle.quantize(img32).astype(np.int16) - oracle.quantize(ref).astype(np.int16)).max(axis=2)
+    assert float((d <= 2).mean()) >= 0.999 and st32["rays"] == 2 * 320 * 240
 
 
 @pytest.mark.parametrize("name", list(CONFIGS))

@@ -1,5 +1,6 @@
 """rt_image_write (canvas.rs:75-137): the 8-bit frame as PNG (RGB8, filter
-None, best deflate, as Canvas::to_png_file) or binary PPM.  Host only."""
+None, best deflate, as Canvas::to_png_file) or the reference's P3 text
+(Canvas::to_ppm_file), byte for byte; binary P6 as an opt-in.  Host only."""
 import numpy as np
 import pytest
 
@@ -34,18 +35,86 @@ def test_png_rows_unfiltered(rtc, tmp_path):
     assert rows[1:19] == img[0].tobytes()
 
 
-def test_ppm(rtc, tmp_path):
-    img = np.random.default_rng(3).integers(0, 256, size=(7, 9, 3), dtype=np.uint8)
+def _reference_canvas_5x3():
+    """canvas.rs:181-188: a 5x3 canvas with three pixels set (f64 colours)."""
+    c = np.zeros((3, 5, 3), dtype=np.float64)
+    c[0, 0] = (1.5, 0, 0)
+    c[1, 2] = (0, 0.5, 0)
+    c[2, 4] = (-0.5, 0, 1)
+    return c
+
+
+def test_ppm_header_kat(rtc, tmp_path):
+    """canvas.rs:171-178: header lines "P3", "5 3", "255"."""
+    path = tmp_path / "h.ppm"
+    rtc.write_image(path, np.zeros((3, 5, 3), dtype=np.uint8))
+    lines = path.read_bytes().decode().split("\n")
+    assert lines[:3] == ["P3", "5 3", "255"]
+
+
+def test_ppm_kat(rtc, tmp_path):
+    """canvas.rs:180-202, byte for byte: the canvas quantized as canvas.rs:81 does
+    (clamp, *255, round half away from zero: 0.5 -> 128), 15 channels per line."""
+    img = rtc.canvas_quantize(_reference_canvas_5x3())
+    path = tmp_path / "kat.ppm"
+    rtc.write_image(path, img)
+    raw = path.read_bytes()
+    expected = ("P3\n5 3\n255\n"
+                "255   0   0   0   0   0   0   0   0   0   0   0   0   0   0\n"
+                "  0   0   0   0   0   0   0 128   0   0   0   0   0   0   0\n"
+                "  0   0   0   0   0   0   0   0   0   0   0   0   0   0 255").encode()
+    assert raw == expected  # no trailing newline (lines joined by "\n")
+
+
+def _p3_reference(img):
+    """canvas.rs:75-97 restated in Python: chunks of 5 pixels across rows."""
+    h, w, _ = img.shape
+    flat = img.reshape(-1, 3)
+    lines = ["P3", f"{w} {h}", "255"]
+    for p in range(0, len(flat), 5):
+        lines.append(" ".join(f"{int(v):>3}" for v in flat[p:p + 5].reshape(-1)))
+    return "\n".join(lines).encode()
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (7, 9), (3, 5), (2, 4), (0, 0)])
+def test_ppm_lines_cross_rows(rtc, tmp_path, shape):
+    """Pixels per line = floor(70 / 12) = 5 regardless of the row length (canvas.rs:76-77)."""
+    img = np.random.default_rng(shape[0] * 10 + shape[1]).integers(0, 256, size=(*shape, 3), dtype=np.uint8)
     path = tmp_path / "frame.ppm"
     rtc.write_image(path, img)
+    assert path.read_bytes() == _p3_reference(img)
+
+
+def test_ppm_binary_opt_in(rtc, tmp_path):
+    img = np.random.default_rng(3).integers(0, 256, size=(7, 9, 3), dtype=np.uint8)
+    path = tmp_path / "frame.ppm"
+    rtc.write_image(path, img, fmt="ppm-binary")
     raw = path.read_bytes()
     head = b"P6\n9 7\n255\n"
     assert raw[:len(head)] == head
     assert np.array_equal(np.frombuffer(raw[len(head):], dtype=np.uint8).reshape(7, 9, 3), img)
 
 
+def test_canvas_quantize(rtc):
+    """canvas.rs:117-123: clamp to [0, 1], *255, round half away from zero, NaN -> 0."""
+    v = np.array([-1.0, 0.0, 0.5 / 255, 0.5, 1.5 / 255, 1.0, 2.0, np.nan, np.inf, -np.inf, 0.25])
+    q = rtc.canvas_quantize(v)
+    assert q.tolist() == [0, 0, 1, 128, 2, 255, 255, 0, 255, 0, 64]
+
+
+def test_parent_dirs_created(rtc, tmp_path):
+    """Canvas::prepare_file (canvas.rs:99-105): create_dir_all on the parent."""
+    for name in ("a/b/c/x.png", "d/e/x.ppm"):
+        path = tmp_path / name
+        rtc.write_image(path, np.zeros((2, 2, 3), dtype=np.uint8))
+        assert path.exists()
+
+
 def test_errors(rtc, tmp_path):
     with pytest.raises(ValueError):
         rtc.write_image(tmp_path / "x.png", np.zeros((2, 2, 3), dtype=np.float32))
-    with pytest.raises(rtc.RenderError):
-        rtc.write_image(tmp_path / "missing_dir" / "x.png", np.zeros((2, 2, 3), dtype=np.uint8))
+    (tmp_path / "file").write_text("")
+    with pytest.raises(rtc.RenderError):  # a parent that is a file
+        rtc.write_image(tmp_path / "file" / "x.png", np.zeros((2, 2, 3), dtype=np.uint8))
+    with pytest.raises(rtc.RenderError):  # PNG of an empty canvas
+        rtc.write_image(tmp_path / "e.png", np.zeros((0, 0, 3), dtype=np.uint8))
