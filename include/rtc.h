@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* Image tile rendered by one workgroup (one wave = one 64-pixel row run, so
  * output stores are contiguous); RT_TILE_H rows are also the row-block unit
@@ -164,6 +164,8 @@ typedef struct rt_camera_desc {
 #define RT_FLAG_NO_SHADE 2u    /* closest hit only, colour = normalised t   */
 #define RT_FLAG_NO_TRACE 4u    /* camera ray only, colour = direction       */
 #define RT_FLAG_STAMPS 8u      /* record per-workgroup start/end timestamps */
+#define RT_FLAG_FAIL_LAUNCH 16u /* fail with RT_ERR_HIP after planning, before
+                                  * the enqueue (tests the error path)      */
 
 typedef struct rt_render_options {
     uint32_t max_depth;    /* `remaining` of the primary ray; 6 = reference */
@@ -296,15 +298,32 @@ int rt_debug_normal(rt_context* ctx, uint32_t shape, const double* points, uint6
 /* Per-scene kernels.  For f32 frames the library compiles (hipRTC), once
  * per uploaded world, the same tracer source with the world's shape table as
  * compile-time constants, and runs it instead of the generic kernel (same
- * pixels, bit for bit).  mode 0 = never, 1 = every f32 frame, 2 = frames of
- * at least 64K pixels (the default; env RTC_JIT=0|1 overrides at context
- * creation).  rt_jit_status: whether the last launch ran a per-scene kernel,
- * the compile milliseconds spent by this context, and the last build error
- * (a failed build keeps the generic kernel for that world).  Builds are
- * also cached on disk across processes: env RTC_JIT_CACHE = a directory, or
- * 0 for none (default $XDG_CACHE_HOME/rtc_jit, else ~/.cache/rtc_jit). */
+ * pixels, bit for bit).  Modes (rt_context_set_jit; env RTC_JIT=0|1|2|3 at
+ * context creation):
+ *   RT_JIT_OFF    never;
+ *   RT_JIT_SYNC   every f32 frame, the build compiled in line on the first
+ *                 one (deterministic: tests);
+ *   RT_JIT_AUTO   the default.  Frames of at least 64K pixels; the build runs
+ *                 on a host thread, started by the SECOND such frame of an
+ *                 uploaded world, and frames render with the generic kernel
+ *                 until it is ready.  A one-shot render (Camera::render, the
+ *                 CLI) never compiles; repeated renders switch once the
+ *                 build lands.  A build already made in this process (or on
+ *                 disk) for the same world is used from the first frame;
+ *   RT_JIT_EAGER  as AUTO, but the first large frame starts the build.
+ * rt_jit_status: whether the last launch ran a per-scene kernel, the compile
+ * (or cache-load) milliseconds of the builds this context started, and the
+ * last build error (a failed build keeps the generic kernel for that world).
+ * rt_jit_wait: block until this context's builds in flight have finished
+ * (at most timeout_ms; < 0 = no limit); *pending = builds still running.
+ * A context destroyed with a build in flight does not wait for it; librtc
+ * joins its build threads when it is unloaded.  Builds are also cached on
+ * disk across processes: env RTC_JIT_CACHE = a directory, or 0 for none
+ * (default $XDG_CACHE_HOME/rtc_jit, else ~/.cache/rtc_jit). */
+enum { RT_JIT_OFF = 0, RT_JIT_SYNC = 1, RT_JIT_AUTO = 2, RT_JIT_EAGER = 3 };
 int rt_context_set_jit(rt_context* ctx, int mode);
 int rt_jit_status(rt_context* ctx, int* used_last_launch, double* compile_ms, char* log, size_t log_len);
+int rt_jit_wait(rt_context* ctx, double timeout_ms, int* pending);
 
 /* Cumulative device counters since context creation (after a sync). */
 int rt_read_counters(rt_context* ctx, rt_stats* totals);

@@ -75,9 +75,9 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "error: %s\n", rt_last_error());
         return 1;
     }
-    // One frame: a per-scene kernel build (0.3-1.3 s of hipRTC, DESIGN.md
-    // §3.3b) would cost far more than it saves on a single render.
-    rt_context_set_jit(ctx, 0);
+    // One frame: the default per-scene policy (RT_JIT_AUTO) starts a hipRTC
+    // build only at a world's second large frame, so this render never
+    // compiles.
     rt_render_options o = {depth, precision, RT_OUT_U8, 0, 1, 0};
     std::vector<uint8_t> img((size_t)cam.width * cam.height * 3);
     rt_stats st;

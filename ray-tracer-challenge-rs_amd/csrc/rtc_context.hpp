@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -38,6 +39,8 @@ struct DeviceWorld {
         lights = nullptr;
     }
 };
+
+struct CodeBuild;  // rtc_jit.cpp: one hipRTC build of a per-scene kernel, possibly in flight
 
 }  // namespace rtc
 
@@ -110,13 +113,18 @@ struct rt_context {
     size_t scratch_bytes = 0;
     // Per-scene f32 kernels (rtc_jit.cpp): the f32 shape table of the last
     // upload, the kernels built for it (direct/pool x global/LDS world), and
-    // RTC_JIT = 0 (never) | 1 (every f32 frame) | auto (frames of at least
-    // kJitMinTiles tiles; small frames are not worth a build)
+    // RTC_JIT / rt_context_set_jit = RT_JIT_OFF | RT_JIT_SYNC | RT_JIT_AUTO
+    // (default) | RT_JIT_EAGER (rtc.h).
     std::vector<rtc::ShapeRec<float>> jit_shapes;
     int32_t jit_begin[rtc::kNumKinds + 1] = {};
     hipFunction_t jit_fn[4] = {};
+    std::shared_ptr<rtc::CodeBuild> jit_build[4];  // the build each variant waits for (host thread)
+    bool jit_rejected[4] = {};   // built, but refused for occupancy or scratch (that variant only)
+    bool jit_owner[4] = {};      // this context started the build: its time goes into jit_compile_ms
+    uint32_t jit_frames = 0;     // large f32 frames of this upload so far (RT_JIT_AUTO starts at the 2nd)
+    std::string arch = "gfx950"; // the device's gfx target (hipDeviceProp_t::gcnArchName), for hipRTC
     int jit_mode = 2;
-    bool jit_failed = false, jit_used = false;
+    bool jit_failed = false, jit_used = false;  // jit_failed: the world's build failed (compile or load)
     double jit_compile_ms = 0;  // compile (or disk-cache load) time of this context's per-scene builds
     int jit_cache_hits = 0;     // builds loaded from the on-disk cache
     std::string jit_log;
@@ -166,6 +174,7 @@ int launch_frame(rt_context* ctx, const rt_camera_desc* cam, const rt_render_opt
 // `static_blocks` workgroups per CU, or null (use the generic kernel)
 constexpr uint32_t kJitMinTiles = 256;  // 64K pixels
 int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int static_blocks, hipFunction_t* fn);
+int jit_wait(rt_context* ctx, double timeout_ms, int* pending);
 
 // rtc_group.cpp: the same entry points on a multi-GPU context
 int group_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats,

@@ -555,11 +555,13 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     // between: two sets alternate, both zeroed at context creation, and each
     // launch zeroes the other set for the next one (trace_pool; the
     // previous user of that set is complete by stream order).
-    if (ls.sched == kSchedDynamic) {
+    // The set flips only once the launch is enqueued: a launch that fails
+    // before that leaves its set unused and still zero for the next one.
+    const bool dynamic = ls.sched == kSchedDynamic;
+    if (dynamic) {
         const size_t set = (size_t)kTileQueues * kQueueStride;
         P.tile_counter = ctx->d_tile_counter + (ctx->head_set ? set : 0);
         P.next_tile_counter = ctx->d_tile_counter + (ctx->head_set ? 0 : set);
-        ctx->head_set ^= 1;
         if (ls.pool && ctx->tile_order && cam) {  // frames only: a ray batch's content is not in the signature
             if ((rc = plan_tile_order<R>(ctx, P, cam, depth, ls.grid, stream))) return rc;
         }
@@ -592,10 +594,12 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     hipFunction_t jf = nullptr;
     if constexpr (sizeof(R) == 4) {
         const bool want = cam && !dup && !(flags & RT_FLAG_STAMPS) &&
-                          (ctx->jit_mode == 1 || (ctx->jit_mode == 2 && P.n_tiles >= kJitMinTiles));
+                          (ctx->jit_mode == RT_JIT_SYNC || (ctx->jit_mode >= RT_JIT_AUTO && P.n_tiles >= kJitMinTiles));
+        if (want) ++ctx->jit_frames;
         if (want && (rc = jit_function(ctx, ls.pool, ls.world_lds != 0, ls.lds, ls.per_cu, &jf))) return rc;
     }
     ctx->jit_used = jf != nullptr;
+    if (flags & RT_FLAG_FAIL_LAUNCH) return set_error(RT_ERR_HIP, "launch refused (RT_FLAG_FAIL_LAUNCH)");
     if (jf) {
         const ShapeRec<R>* sh = P.scene.shapes;
         const MaterialRec<R>* mt = P.scene.materials;
@@ -604,6 +608,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
         void* args[] = {&P, &sh, &mt, &pt, &lt};
         (void)hipGetLastError();
         RT_HIP(hipModuleLaunchKernel(jf, ls.grid, 1, 1, kBlock, 1, 1, (unsigned)ls.lds, stream, args, nullptr));
+        if (dynamic) ctx->head_set ^= 1;
         return RT_OK;
     }
     if (hipError_t e = sp ? sp::launch_trace<R>(P, ls.pool, dup, ls.grid, ls.lds, stream)
@@ -613,6 +618,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
                                          std::to_string(ls.grid) + ", dynamic LDS " + std::to_string(ls.lds) +
                                          " B, pool " + std::to_string(ls.lcap) + "/" + std::to_string(ls.cap) +
                                          " rays in LDS): " + hipGetErrorString(e));
+    if (dynamic) ctx->head_set ^= 1;
     return RT_OK;
 }
 
@@ -745,6 +751,10 @@ int create_device_context(int device_ordinal, rt_context** out) {
     hipDeviceProp_t prop;
     RT_HIP(hipGetDeviceProperties(&prop, device_ordinal));
     ctx->cu_count = prop.multiProcessorCount;
+    {  // "gfx950:sramecc+:xnack-" -> "gfx950": the per-scene builds' target
+        const std::string a(prop.gcnArchName);
+        if (!a.empty()) ctx->arch = a.substr(0, a.find(':'));
+    }
     ctx->lds_per_block = prop.sharedMemPerBlock;  // launch limit of static + dynamic LDS
     // scheduling knobs: "grid" (one workgroup per tile, the hardware dispatcher
     // balances), "static" (resident grid, fixed tile stride) or "dynamic"
@@ -767,7 +777,8 @@ int create_device_context(int device_ordinal, rt_context** out) {
     if (const char* e = std::getenv("RTC_SPLIT")) ctx->split_factor = std::atof(e);
     if (const char* e = std::getenv("RTC_ORDER_BUILDS")) ctx->order_max_builds = std::atoi(e);
     if (const char* e = std::getenv("RTC_DIRECT_GRID")) ctx->direct_grid = (uint32_t)std::atoi(e);
-    if (const char* e = std::getenv("RTC_JIT")) ctx->jit_mode = !std::strcmp(e, "0") ? 0 : !std::strcmp(e, "1") ? 1 : 2;
+    if (const char* e = std::getenv("RTC_JIT"))
+        ctx->jit_mode = (e[0] >= '0' && e[0] <= '3' && !e[1]) ? e[0] - '0' : RT_JIT_AUTO;
     RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreate(&ctx->ev_start));
     RT_HIP(hipEventCreate(&ctx->ev_stop));
@@ -857,7 +868,12 @@ int capture_jit_table(rt_context* ctx) {
     ctx->jit_shapes.assign(n, ShapeRec<float>{});
     if (n) RT_HIP(hipMemcpy(ctx->jit_shapes.data(), ctx->w32.shapes, n * sizeof(ShapeRec<float>), hipMemcpyDeviceToHost));
     for (int k = 0; k <= kNumKinds; ++k) ctx->jit_begin[k] = ctx->w32.scene.kind_begin[k];
-    for (auto& f : ctx->jit_fn) f = nullptr;
+    for (int v = 0; v < 4; ++v) {
+        ctx->jit_fn[v] = nullptr;
+        ctx->jit_build[v].reset();
+        ctx->jit_rejected[v] = ctx->jit_owner[v] = false;
+    }
+    ctx->jit_frames = 0;
     ctx->jit_failed = false;
     ctx->jit_log.clear();
     return RT_OK;
@@ -1046,7 +1062,7 @@ int rt_debug_normal(rt_context* ctx, uint32_t shape, const double* points, uint6
 }
 
 int rt_context_set_jit(rt_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 2) return set_error(RT_ERR_INVALID, "bad arguments");
+    if (!ctx || mode < RT_JIT_OFF || mode > RT_JIT_EAGER) return set_error(RT_ERR_INVALID, "bad arguments");
     ctx->jit_mode = mode;
     for (rt_context* p : ctx->peers) p->jit_mode = mode;
     return RT_OK;
@@ -1060,6 +1076,18 @@ int rt_jit_status(rt_context* ctx, int* used_last_launch, double* compile_ms, ch
         std::strncpy(log, ctx->jit_log.c_str(), log_len - 1);
         log[log_len - 1] = '\0';
     }
+    return RT_OK;
+}
+
+int rt_jit_wait(rt_context* ctx, double timeout_ms, int* pending) {
+    if (!ctx) return set_error(RT_ERR_INVALID, "null context");
+    int total = 0, left = 0;
+    for (rt_context* c : ctx->peers) {
+        jit_wait(c, timeout_ms, &left);
+        total += left;
+    }
+    jit_wait(ctx, timeout_ms, &left);
+    if (pending) *pending = total + left;
     return RT_OK;
 }
 

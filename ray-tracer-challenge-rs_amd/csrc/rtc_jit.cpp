@@ -11,18 +11,26 @@
 // operations on the same values, so frames are bit-identical to the generic
 // kernel (tests/test_gpu_jit.py); only the f32 frame kernels are built this
 // way (the f64 parity path, rt_color_at and small frames keep the generic
-// kernels).  Builds are cached per process by table content and device, and
-// on disk by everything the compiler sees (source, scene header, options,
-// hipRTC version), so a later process loads the code object instead of
-// compiling it (RTC_JIT_CACHE: a directory, or 0 for none; default
-// $XDG_CACHE_HOME/rtc_jit or ~/.cache/rtc_jit).  A failed build falls back to
-// the generic kernel for that world.
+// kernels).  Builds are cached per process by table content (code objects)
+// and device (loaded modules), and on disk by everything the compiler sees
+// (source, scene header, options, the build's defines, hipRTC / HIP versions
+// and the identity of librtc, libhiprtc and comgr), so a later process loads
+// the code object instead of compiling it (RTC_JIT_CACHE: a directory, or 0
+// for none; default $XDG_CACHE_HOME/rtc_jit or ~/.cache/rtc_jit).
+//
+// Off the frame's critical path (RT_JIT_AUTO, the default): the compile runs
+// on a host thread; frames keep the generic kernel until it has landed, then
+// the next frame loads the module and switches (same pixels either way).  A
+// failed compile or module load keeps the generic kernel for that world; a
+// build refused for occupancy or scratch keeps it for that variant only.
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cerrno>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -30,8 +38,11 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
+#include <dirent.h>
+#include <dlfcn.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -89,6 +100,19 @@ struct CodeObject {
     bool from_disk = false;
     uint64_t key = 0;  // the disk cache key (every input of the compile)
 };
+
+}  // namespace
+
+// One per-scene kernel build: the code object of (world table, variant),
+// compiled on a host thread (or in line for RT_JIT_SYNC) and shared by every
+// context of the process that uploads the same world.
+struct CodeBuild {
+    std::atomic<int> state{0};  // 0 compiling, 1 ready, 2 failed
+    CodeObject co;
+    std::string log;
+};
+
+namespace {
 
 // ------------------------------------------------------- on-disk code cache
 // One file per build: "RTCJIT2\n" <lowered name> "\n" <code bytes> " "
@@ -162,13 +186,85 @@ void cache_store(const std::string& dir, const std::string& path, const CodeObje
     if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
 }
 
-// Process-wide caches: code objects by (table, kernel); loaded functions by
-// (code object, device).
-std::mutex g_mu;
-std::map<std::pair<uint64_t, int>, std::shared_ptr<CodeObject>> g_code;
-std::map<std::pair<uint64_t, int>, std::pair<hipModule_t, hipFunction_t>> g_fn;
+// Identity of a shared object: path, size and modification time.
+uint64_t file_identity(const char* path, uint64_t h) {
+    struct stat st;
+    if (!path || ::stat(path, &st) != 0) return fnv("?", 1, h);
+    h = fnv(path, std::strlen(path) + 1, h);
+    const int64_t v[2] = {(int64_t)st.st_size, (int64_t)st.st_mtime};
+    return fnv(v, sizeof v, h);
+}
 
-int compile(const std::string& scene, const char* name, CodeObject& out, std::string& log, bool use_cache = true) {
+// The toolchain and library behind a build, for the disk cache key: hipRTC
+// and HIP runtime versions, and the identity of librtc itself, of libhiprtc
+// and of the comgr libraries next to it (the compiler proper), so a rebuilt
+// librtc or an updated compiler within the same hipRTC minor version never
+// loads code objects made by the old one.
+uint64_t toolchain_identity() {
+    static const uint64_t id = [] {
+        uint64_t h = 1469598103934665603ull;
+        int v[4] = {};
+        hiprtcVersion(&v[0], &v[1]);
+        (void)hipRuntimeGetVersion(&v[2]);
+        (void)hipDriverGetVersion(&v[3]);
+        h = fnv(v, sizeof v, h);
+        Dl_info self{}, rtcc{};
+        if (dladdr(reinterpret_cast<void*>(&toolchain_identity), &self)) h = file_identity(self.dli_fname, h);
+        if (dladdr(reinterpret_cast<void*>(&hiprtcCompileProgram), &rtcc) && rtcc.dli_fname) {
+            h = file_identity(rtcc.dli_fname, h);
+            std::string dir(rtcc.dli_fname);
+            dir = dir.substr(0, dir.find_last_of('/') + 1);
+            if (DIR* d = ::opendir(dir.empty() ? "." : dir.c_str())) {
+                std::vector<std::string> names;
+                while (dirent* e = ::readdir(d))
+                    if (std::strstr(e->d_name, "amd_comgr")) names.push_back(e->d_name);
+                ::closedir(d);
+                std::sort(names.begin(), names.end());
+                for (const std::string& n : names) h = file_identity((dir + n).c_str(), h);
+            }
+        }
+        return h;
+    }();
+    return id;
+}
+
+// Process-wide caches: builds by (table, kernel variant); loaded functions
+// by (build, device).  Build threads are joined when librtc is unloaded (the
+// registry is declared last, so it is destroyed first).
+std::mutex g_mu;
+std::condition_variable g_cv;  // a build finished
+std::map<std::pair<uint64_t, int>, std::shared_ptr<CodeBuild>> g_code;
+std::map<std::pair<uint64_t, int>, std::pair<hipModule_t, hipFunction_t>> g_fn;
+struct BuildThreads {
+    std::mutex mu;
+    std::vector<std::thread> threads;
+    ~BuildThreads() {
+        std::lock_guard<std::mutex> lk(mu);
+        for (std::thread& t : threads)
+            if (t.joinable()) t.join();
+    }
+    void add(std::thread t) {
+        std::lock_guard<std::mutex> lk(mu);
+        threads.push_back(std::move(t));
+    }
+} g_threads;
+
+// The static build's EXTRA flags (Makefile), passed on to hipRTC: -D/-U only.
+std::vector<std::string> build_defines() {
+    std::vector<std::string> out;
+    const std::string all(kBuildExtra);
+    for (size_t p = 0; p < all.size();) {
+        size_t q = all.find_first_of(" \t\n", p);
+        if (q == std::string::npos) q = all.size();
+        const std::string tok = all.substr(p, q - p);
+        if (tok.size() > 2 && tok[0] == '-' && (tok[1] == 'D' || tok[1] == 'U')) out.push_back(tok);
+        p = q + 1;
+    }
+    return out;
+}
+
+int compile(const std::string& scene, const char* name, const std::string& arch, CodeObject& out, std::string& log,
+            bool use_cache = true) {
     const std::string main_src = std::string("#define RTC_JIT 1\n#include \"rtc_jit_scene.hpp\"\n") + kSrcKernels;
     const char* headers[] = {scene.c_str(), kSrcInternal, kSrcRtcH};
     const char* names[] = {"rtc_jit_scene.hpp", "rtc_internal.hpp", "../../include/rtc.h"};
@@ -182,21 +278,14 @@ int compile(const std::string& scene, const char* name, CodeObject& out, std::st
     // values computed from them) out of the generation and tile loops, where
     // they are held across the loop and spill (reflect_refract's pool kernel:
     // 100 B/lane of scratch and 106 SGPRs with it, 8 B and 73 VGPRs without).
-    // A build that overrides the kernels' tuning macros (Makefile EXTRA)
-    // passes them on, so both builds plan the same occupancy.
-    std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3",    "-std=c++20", "-ffp-contract=off",
-                                     "-fno-slp-vectorize",    "-mllvm", "-disable-machine-licm"};
-#define RTC_STR2(x) #x
-#define RTC_STR(x) RTC_STR2(x)
-#ifdef RTC_POOL_WAVES
-    opts.push_back("-DRTC_POOL_WAVES=" RTC_STR(RTC_POOL_WAVES));
-#endif
-#ifdef RTC_DIRECT_WAVES
-    opts.push_back("-DRTC_DIRECT_WAVES=" RTC_STR(RTC_DIRECT_WAVES));
-#endif
-#ifdef RTC_WAVE_W
-    opts.push_back("-DRTC_WAVE_W=" RTC_STR(RTC_WAVE_W));
-#endif
+    // The device's own gfx target.  A build with defines of its own
+    // (Makefile EXTRA: tuning macros, f32 math variants) passes all of them
+    // on, so both builds run the same arithmetic and plan the same occupancy.
+    const std::string arch_opt = "--offload-arch=" + arch;
+    std::vector<const char*> opts = {arch_opt.c_str(),     "-O3",    "-std=c++20", "-ffp-contract=off",
+                                     "-fno-slp-vectorize", "-mllvm", "-disable-machine-licm"};
+    static const std::vector<std::string> defines = build_defines();
+    for (const std::string& d : defines) opts.push_back(d.c_str());
     // The direct kernel fences the ray at every third shape only: the shape
     // tests in between may interleave (more ILP) and still fit 8 waves/SIMD
     // without spilling.  Same-box A/B against a fence per shape: shadow_puppets
@@ -215,15 +304,13 @@ int compile(const std::string& scene, const char* name, CodeObject& out, std::st
         }
     }
     for (const std::string& x : extra) opts.push_back(x.c_str());
-    // the disk cache key: every input of the compile
-    int vmaj = 0, vmin = 0;
-    hiprtcVersion(&vmaj, &vmin);
+    // the disk cache key: every input of the compile, and the toolchain
     uint64_t key = fnv(main_src.data(), main_src.size());
     for (const char* h : headers) key = fnv(h, std::strlen(h) + 1, key);
     for (const char* o : opts) key = fnv(o, std::strlen(o) + 1, key);
     key = fnv(name, std::strlen(name) + 1, key);
-    const int ver[2] = {vmaj, vmin};
-    key = fnv(ver, sizeof ver, key);
+    const uint64_t tool = toolchain_identity();
+    key = fnv(&tool, sizeof tool, key);
     out.key = key;
     const std::string dir = cache_dir();
     const std::string path = dir.empty() || !use_cache ? std::string() : cache_path(dir, key);
@@ -272,52 +359,113 @@ int compile(const std::string& scene, const char* name, CodeObject& out, std::st
     return rc;
 }
 
+// Compile one build (host thread or in line) and publish it.
+void run_build(std::shared_ptr<CodeBuild> b, std::string scene, std::string name, std::string arch) {
+    std::string log;
+    const int rc = compile(scene, name.c_str(), arch, b->co, log);
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (rc) b->log = std::string(rt_last_error());
+        b->state.store(rc ? 2 : 1, std::memory_order_release);
+    }
+    g_cv.notify_all();
+}
+
 }  // namespace
 
 // The per-scene kernel for this context's uploaded world, or null (use the
-// generic kernel): compiled on first use per world and kernel variant.
+// generic kernel this launch).  RT_JIT_SYNC compiles in line; RT_JIT_AUTO /
+// RT_JIT_EAGER start the compile on a host thread at the 2nd / 1st large
+// frame of an upload and return null until it has landed.
 int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int static_blocks, hipFunction_t* fn) {
     *fn = nullptr;
     if (ctx->jit_failed || ctx->jit_shapes.empty()) return RT_OK;
-
     const int variant = (pool ? 2 : 0) + (lds ? 1 : 0);
     if (ctx->jit_fn[variant]) {
         *fn = ctx->jit_fn[variant];
         return RT_OK;
     }
-    const uint64_t key = fnv(ctx->jit_begin, sizeof ctx->jit_begin,
-                             fnv(ctx->jit_shapes.data(), ctx->jit_shapes.size() * sizeof(ShapeRec<float>)));
-    std::shared_ptr<CodeObject> co;
-    std::string log;
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        auto it = g_code.find({key, variant});
-        if (it != g_code.end()) co = it->second;
-    }
-    if (!co) {
-        auto built = std::make_shared<CodeObject>();
-        if (compile(scene_header(ctx->jit_shapes, ctx->jit_begin), kernel_name(pool, lds), *built, log)) {
-            ctx->jit_failed = true;  // keep the generic kernel for this world
-            ctx->jit_log = rt_last_error();
-            return RT_OK;
+    if (ctx->jit_rejected[variant]) return RT_OK;
+    std::shared_ptr<CodeBuild>& b = ctx->jit_build[variant];
+    if (!b) {
+        const uint64_t key = fnv(ctx->jit_begin, sizeof ctx->jit_begin,
+                                 fnv(ctx->jit_shapes.data(), ctx->jit_shapes.size() * sizeof(ShapeRec<float>)));
+        const bool sync = ctx->jit_mode == RT_JIT_SYNC;
+        const uint32_t start_at = ctx->jit_mode == RT_JIT_AUTO ? 2 : 1;
+        bool start = false;
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            auto it = g_code.find({key, variant});
+            if (it != g_code.end()) {
+                b = it->second;  // built (or building, or failed) for another context or an earlier upload
+            } else if (sync || ctx->jit_frames >= start_at) {
+                b = std::make_shared<CodeBuild>();
+                g_code[{key, variant}] = b;
+                start = true;
+            }
         }
-        ctx->jit_compile_ms += built->compile_ms;
-        if (built->from_disk) ++ctx->jit_cache_hits;
-        std::lock_guard<std::mutex> lk(g_mu);
-        co = g_code.emplace(std::make_pair(key, variant), built).first->second;
+        if (!b) return RT_OK;
+        if (start) {
+            ctx->jit_owner[variant] = true;
+            std::string scene = scene_header(ctx->jit_shapes, ctx->jit_begin);
+            if (sync) {
+                run_build(b, std::move(scene), kernel_name(pool, lds), ctx->arch);
+            } else {
+                try {
+                    g_threads.add(std::thread(run_build, b, std::move(scene), std::string(kernel_name(pool, lds)),
+                                              ctx->arch));
+                } catch (const std::exception& e) {  // no thread: build in line instead
+                    run_build(b, scene_header(ctx->jit_shapes, ctx->jit_begin), kernel_name(pool, lds), ctx->arch);
+                }
+            }
+        }
+    }
+    if (ctx->jit_mode == RT_JIT_SYNC) {  // wait for a build another context started
+        std::unique_lock<std::mutex> lk(g_mu);
+        g_cv.wait(lk, [&] { return b->state.load() != 0; });
+    }
+    const int state = b->state.load(std::memory_order_acquire);
+    if (state == 0) return RT_OK;  // still compiling: the generic kernel this frame
+    if (ctx->jit_owner[variant]) {
+        ctx->jit_compile_ms += b->co.compile_ms;
+        if (b->co.from_disk) ++ctx->jit_cache_hits;
+        ctx->jit_owner[variant] = false;
+    }
+    if (state == 2) {
+        ctx->jit_failed = true;  // keep the generic kernel for this world
+        ctx->jit_log = b->log;
+        return RT_OK;
     }
     std::pair<hipModule_t, hipFunction_t> mf{};
     {
         std::lock_guard<std::mutex> lk(g_mu);
-        auto it = g_fn.find({(uint64_t)(uintptr_t)co.get(), ctx->device});
+        auto it = g_fn.find({(uint64_t)(uintptr_t)b.get(), ctx->device});
         if (it != g_fn.end()) mf = it->second;
     }
     if (!mf.second) {
+        // a code object the device cannot load (another target, a damaged
+        // build) fails like a failed compile: the generic kernel, not an error
         RT_HIP(hipSetDevice(ctx->device));
-        RT_HIP(hipModuleLoadData(&mf.first, co->code.data()));
-        RT_HIP(hipModuleGetFunction(&mf.second, mf.first, co->lowered.c_str()));
+        hipError_t e = hipModuleLoadData(&mf.first, b->co.code.data());
+        if (e == hipSuccess) {
+            e = hipModuleGetFunction(&mf.second, mf.first, b->co.lowered.c_str());
+            if (e != hipSuccess) {
+                (void)hipModuleUnload(mf.first);
+                mf = {};
+            }
+        }
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            ctx->jit_failed = true;
+            ctx->jit_log = std::string("per-scene kernel not loaded (") + ctx->arch + "): " + hipGetErrorString(e);
+            return RT_OK;
+        }
         std::lock_guard<std::mutex> lk(g_mu);
-        g_fn[{(uint64_t)(uintptr_t)co.get(), ctx->device}] = mf;
+        auto ins = g_fn.emplace(std::make_pair((uint64_t)(uintptr_t)b.get(), ctx->device), mf);
+        if (!ins.second) {  // another context of this device loaded it meanwhile
+            (void)hipModuleUnload(mf.first);
+            mf = ins.first->second;
+        }
     }
     // The launch is planned with the generic kernel's occupancy: use the
     // per-scene kernel only if it keeps at least as many workgroups per CU,
@@ -325,18 +473,34 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
     // 16 B/lane, e.g. cylinders: 12 B/lane, values reloaded once per tile,
     // 0.15 ms against 0.19 ms for the generic kernel).  A build with real
     // spills ran slower than the generic kernel (shadow_puppets before the
-    // ray fence: 56 B/lane, +10 %).
+    // ray fence: 56 B/lane, +10 %).  A refusal holds for this variant only.
     int blocks = 0, scratch = 0;
     RT_HIP(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mf.second, kBlock, dyn_lds));
     RT_HIP(hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, mf.second));
     if (blocks < static_blocks || scratch > (pool ? 16 : 0)) {
-        ctx->jit_failed = true;
-        ctx->jit_log = "per-scene kernel not used: " + std::to_string(blocks) + " workgroups/CU (generic " +
-                       std::to_string(static_blocks) + "), " + std::to_string(scratch) + " B/lane of scratch";
+        ctx->jit_rejected[variant] = true;
+        ctx->jit_log = std::string("per-scene ") + (pool ? "pool" : "direct") + " kernel not used: " +
+                       std::to_string(blocks) + " workgroups/CU (generic " + std::to_string(static_blocks) + "), " +
+                       std::to_string(scratch) + " B/lane of scratch";
         return RT_OK;
     }
     ctx->jit_fn[variant] = mf.second;
     *fn = mf.second;
+    return RT_OK;
+}
+
+// Block until this context's builds in flight have finished (rt_jit_wait).
+int jit_wait(rt_context* ctx, double timeout_ms, int* pending) {
+    const auto deadline = std::chrono::steady_clock::now() +
+                          std::chrono::microseconds((int64_t)(timeout_ms < 0 ? 3.6e9 * 1e3 : timeout_ms * 1e3));
+    auto left = [ctx] {
+        int n = 0;
+        for (const auto& b : ctx->jit_build) n += b && b->state.load() == 0;
+        return n;
+    };
+    std::unique_lock<std::mutex> lk(g_mu);
+    g_cv.wait_until(lk, deadline, [&] { return left() == 0; });
+    if (pending) *pending = left();
     return RT_OK;
 }
 

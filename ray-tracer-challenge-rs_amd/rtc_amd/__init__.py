@@ -30,7 +30,7 @@ __all__ = [
     "RT_DEFAULT_MAX_DEPTH", "RT_TILE_H", "RT_TILE_W",
 ]
 
-RT_ABI_VERSION = 2  # rtc.h; rt_abi_version() must agree (checked at load)
+RT_ABI_VERSION = 3  # rtc.h; rt_abi_version() must agree (checked at load)
 RT_TILE_W = 64
 RT_TILE_H = 4
 RT_DEFAULT_MAX_DEPTH = 6  # World::MAX_REFLECTION_ITERATIONS, world.rs:15
@@ -45,7 +45,8 @@ SHAPE_KINDS = {"sphere": 0, "plane": 1, "cube": 2, "cylinder": 3, "cone": 4, "tr
 PATTERN_KINDS = {"stripe": 0, "gradient": 1, "ring": 2, "checker": 3, "complex": 4, "test": 5}
 PRECISIONS = {"f32": 0, "f64": 1}
 # rt_render_options.flags: diagnostic ablations (rtc.h); never in a parity or bench result
-RT_FLAG_NO_COUNTERS, RT_FLAG_NO_SHADE, RT_FLAG_NO_TRACE, RT_FLAG_STAMPS = 1, 2, 4, 8
+RT_FLAG_NO_COUNTERS, RT_FLAG_NO_SHADE, RT_FLAG_NO_TRACE, RT_FLAG_STAMPS, RT_FLAG_FAIL_LAUNCH = 1, 2, 4, 8, 16
+RT_JIT_OFF, RT_JIT_SYNC, RT_JIT_AUTO, RT_JIT_EAGER = 0, 1, 2, 3
 OUT_FORMATS = {"real": 0, "u8": 1}
 
 
@@ -182,6 +183,7 @@ def _load() -> C.CDLL:
         "rt_context_group": (C.c_int, [C.c_void_p, P(C.c_int), P(C.c_int), P(C.c_int)]),
         "rt_context_set_jit": (C.c_int, [C.c_void_p, C.c_int]),
         "rt_jit_status": (C.c_int, [C.c_void_p, P(C.c_int), P(C.c_double), C.c_char_p, C.c_size_t]),
+        "rt_jit_wait": (C.c_int, [C.c_void_p, C.c_double, P(C.c_int)]),
         "rt_debug_intersect": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), C.c_uint64, C.c_uint32, C.c_uint32,
                                          P(C.c_double)]),
         "rt_debug_normal": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), C.c_uint64, C.c_uint32, C.c_uint32,
@@ -204,7 +206,7 @@ EXPORTED_SYMBOLS = (
     "rt_scene_upload", "rt_shard_rows", "rt_render", "rt_render_device", "rt_color_at", "rt_read_counters",
     "rt_debug_stamps", "rt_debug_tile_costs", "rt_debug_intersect", "rt_debug_normal", "rt_camera_set_transform",
     "rt_shard_row_map", "rt_context_create_multi", "rt_comm_unique_id", "rt_context_create_rank", "rt_context_group",
-    "rt_context_set_jit", "rt_jit_status",
+    "rt_context_set_jit", "rt_jit_status", "rt_jit_wait",
     "rt_assemble_shards", "rt_scene_load_yaml", "rt_scene_load_yaml_text", "rt_scene_view_get", "rt_scene_free",
     "rt_camera_make", "rt_camera_resize", "rt_matrix_inverse", "rt_image_write", "rt_image_write_format",
     "rt_canvas_quantize",
@@ -410,8 +412,16 @@ class Context:
             pass
 
     def set_jit(self, mode: int) -> None:
-        """Per-scene kernels: 0 never, 1 every f32 frame, 2 frames of >= 64K pixels (rtc.h rt_context_set_jit)."""
+        """Per-scene kernels (rtc.h rt_context_set_jit): 0 never, 1 every f32 frame (built in line),
+        2 frames of >= 64K pixels, built on a host thread from the 2nd such frame (the default),
+        3 the same from the 1st."""
         _check(_lib.rt_context_set_jit(self._h, mode))
+
+    def jit_wait(self, timeout_ms: float = -1.0) -> int:
+        """Wait for this context's per-scene builds in flight; returns how many are still running."""
+        n = C.c_int(0)
+        _check(_lib.rt_jit_wait(self._h, float(timeout_ms), C.byref(n)))
+        return n.value
 
     def jit_status(self) -> dict:
         """Whether the last launch ran a per-scene kernel, compile ms so far, last build error."""

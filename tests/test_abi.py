@@ -42,7 +42,7 @@ def test_python_mirror_lists_every_symbol(rtc):
 
 
 def test_abi_version_and_last_error(rtc):
-    assert rtc.abi_version() == rtc.RT_ABI_VERSION == 2
+    assert rtc.abi_version() == rtc.RT_ABI_VERSION == 3
     lib = C.CDLL(LIB)
     lib.rt_last_error.restype = C.c_char_p
     assert lib.rt_last_error() is not None

@@ -78,15 +78,111 @@ def test_per_scene_kernel_all_kinds(gpu_ctx):
         assert np.array_equal(a, b) and _counts(sa) == _counts(sb)
 
 
-def test_default_threshold_uses_the_per_scene_kernel_for_large_frames(gpu_ctx, rtc):
-    scene = scene_fixture("three_sphere_scene")
+def _fresh_world(rtc, name, salt):
+    """A scene whose shape table no earlier test uploaded (the per-process
+    build cache would otherwise hand over a finished build at once): the
+    reference scene plus one tiny sphere far behind the camera."""
+    import ctypes as C
+    scene = scene_fixture(name)
+    n = len(scene.shapes)
+    shapes = (rtc.ShapeDesc * (n + 1))()
+    C.memmove(shapes, scene.shapes, n * C.sizeof(rtc.ShapeDesc))
+    extra = shapes[n]
+    C.pointer(extra)[0] = scene.shapes[0]
+    extra.kind = rtc.SHAPE_KINDS["sphere"]
+    # inverse of translation(0, 1000 + salt, -1e4) * scaling(0.01, 0.01, 0.01)
+    inv = [100.0, 0, 0, 0, 0, 100.0, 0, -100.0 * (1000.0 + salt), 0, 0, 100.0, 1e6, 0, 0, 0, 1.0]
+    for i, v in enumerate(inv):
+        extra.inverse[i] = v
+    scene.shapes = shapes
+    return scene
+
+
+def test_auto_mode_builds_off_the_frame_path(rtc):
+    """RT_JIT_AUTO (the default): the first large frame of an upload renders
+    with the generic kernel and starts nothing (a one-shot render never
+    compiles); the second starts the build on a host thread and still renders
+    generic; once the build lands the next frame switches.  Every frame,
+    before and after the switch, is the same bit for bit."""
+    import time
+    scene = _fresh_world(rtc, "three_sphere_scene", 1.0)
+    cam = rtc.camera_resize(scene.camera, 640, 480)
+    with rtc.Context(0) as ctx:
+        ctx.upload(scene)
+        ctx.render(rtc.camera_resize(scene.camera, 64, 64), 6, precision="f32")  # small: never built
+        t = time.perf_counter()
+        a, sa = ctx.render(cam, 6, precision="f32")
+        first_ms = (time.perf_counter() - t) * 1e3
+        assert not ctx.jit_status()["used"] and ctx.jit_status()["compile_ms"] == 0
+        assert ctx.jit_wait(0) == 0  # the first large frame started no build
+        t = time.perf_counter()
+        b, sb = ctx.render(cam, 6, precision="f32")  # starts the build, renders generic
+        second_ms = (time.perf_counter() - t) * 1e3
+        assert not ctx.jit_status()["used"]
+        assert ctx.jit_wait(60000) == 0
+        c, sc = ctx.render(cam, 6, precision="f32")
+        st = ctx.jit_status()
+        assert st["used"], st["log"][:2000]
+        assert st["compile_ms"] > 0
+        assert np.array_equal(a, b) and np.array_equal(a, c)
+        assert _counts(sa) == _counts(sb) == _counts(sc)
+        # neither generic frame waited for hipRTC (a build takes 300-1300 ms)
+        assert first_ms < 250 and second_ms < 250, (first_ms, second_ms)
+        ctx.render(cam, 6, precision="f64")
+        assert not ctx.jit_status()["used"]  # the f64 parity path is never rebuilt
+
+
+def test_eager_mode_and_reupload_reuse(rtc):
+    """RT_JIT_EAGER starts the build at the first large frame; a re-upload of
+    the same world (another context too) picks the finished build up at once."""
+    scene = _fresh_world(rtc, "shadow_puppets", 2.0)
+    cam = rtc.camera_resize(scene.camera, 640, 480)
+    with rtc.Context(0) as ctx:
+        ctx.set_jit(rtc.RT_JIT_EAGER)
+        ctx.upload(scene)
+        a, _ = ctx.render(cam, 6, precision="f32")
+        assert ctx.jit_wait(60000) == 0
+        b, _ = ctx.render(cam, 6, precision="f32")
+        assert ctx.jit_status()["used"] and np.array_equal(a, b)
+    with rtc.Context(0) as ctx:  # default mode, a new context: the process already holds the build
+        ctx.upload(scene)
+        c, _ = ctx.render(cam, 6, precision="f32")
+        assert ctx.jit_status()["used"] and np.array_equal(a, c)
+        assert ctx.jit_status()["compile_ms"] == 0  # built by the other context
+
+
+def test_destroy_with_a_build_in_flight(rtc):
+    """A context destroyed while its build compiles does not wait for it and
+    leaves nothing broken: the build lands for the next context of the world."""
+    scene = _fresh_world(rtc, "three_sphere_scene", 3.0)
+    cam = rtc.camera_resize(scene.camera, 640, 480)
+    ctx = rtc.Context(0)
+    ctx.set_jit(rtc.RT_JIT_EAGER)
+    ctx.upload(scene)
+    a, _ = ctx.render(cam, 6, precision="f32")
+    ctx.close()
+    with rtc.Context(0) as c2:
+        c2.set_jit(rtc.RT_JIT_SYNC)  # waits for the build in flight instead of starting another
+        c2.upload(scene)
+        b, _ = c2.render(cam, 6, precision="f32")
+        assert c2.jit_status()["used"] and np.array_equal(a, b)
+
+
+def test_failed_launch_keeps_the_queue_heads(gpu_ctx, rtc):
+    """A pool launch that fails after planning (RT_FLAG_FAIL_LAUNCH) must not
+    consume a set of queue heads: the next frame is complete and equal."""
+    scene = scene_fixture("reflect_refract")
+    cam = rtc.camera_resize(scene.camera, 320, 200)
     gpu_ctx.upload(scene)
-    gpu_ctx.render(rtc.camera_resize(scene.camera, 64, 64), 6, precision="f32")
-    assert not gpu_ctx.jit_status()["used"]
-    gpu_ctx.render(rtc.camera_resize(scene.camera, 640, 480), 6, precision="f32")
-    assert gpu_ctx.jit_status()["used"]
-    gpu_ctx.render(rtc.camera_resize(scene.camera, 640, 480), 6, precision="f64")
-    assert not gpu_ctx.jit_status()["used"]  # the f64 parity path is never rebuilt
+    a, sa = gpu_ctx.render(cam, 6, precision="f32")
+    import torch
+    img = torch.zeros((cam.height, cam.width, 3), dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        with pytest.raises(rtc.RenderError):
+            gpu_ctx.render_device(cam, img.data_ptr(), s, 6, "f32", "real", (0, 1), rtc.RT_FLAG_FAIL_LAUNCH)
+        b, sb = gpu_ctx.render(cam, 6, precision="f32")
+        assert np.array_equal(a, b) and _counts(sa) == _counts(sb)
 
 
 _CACHE_PROBE = r"""
