@@ -11,18 +11,23 @@
 // operations on the same values, so frames are bit-identical to the generic
 // kernel (tests/test_gpu_jit.py); only the f32 frame kernels are built this
 // way (the f64 parity path, rt_color_at and small frames keep the generic
-// kernels).  Builds are cached per process by table content (code objects)
-// and device (loaded modules), and on disk by everything the compiler sees
-// (source, scene header, options, the build's defines, hipRTC / HIP versions
-// and the identity of librtc, libhiprtc and comgr), so a later process loads
-// the code object instead of compiling it (RTC_JIT_CACHE: a directory, or 0
-// for none; default $XDG_CACHE_HOME/rtc_jit or ~/.cache/rtc_jit).
+// kernels).
 //
-// Off the frame's critical path (RT_JIT_AUTO, the default): the compile runs
-// on a host thread; frames keep the generic kernel until it has landed, then
-// the next frame loads the module and switches (same pixels either way).  A
-// failed compile or module load keeps the generic kernel for that world; a
-// build refused for occupancy or scratch keeps it for that variant only.
+// The compile runs in a child process (rtc_jitc, next to librtc.so; env
+// RTC_JITC overrides), never on a thread of the render process: a hipRTC
+// compile on a thread raced the host's exit (rtc_jitc.cpp).  RT_JIT_AUTO
+// (the default) starts it at a world's second large frame and keeps the
+// generic kernel until it has landed; a thread of this process only waits
+// for the child (pipe + waitpid) and is detached, so nothing ever has to be
+// joined.  Builds are cached per process by table content (code objects) and
+// device (loaded modules), and on disk by everything the compiler sees
+// (source, scene header, options including the build's own defines, and the
+// toolchain: hipRTC / HIP versions and the identity of librtc, libhiprtc and
+// comgr), so a later process loads the code object instead of compiling it
+// (RTC_JIT_CACHE: a directory, or 0 for none; default $XDG_CACHE_HOME/rtc_jit
+// or ~/.cache/rtc_jit).  A failed compile or module load keeps the generic
+// kernel for that world; a build refused for occupancy or scratch keeps it
+// for that variant only.
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
@@ -43,14 +48,34 @@
 
 #include <dirent.h>
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <spawn.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include "rtc_context.hpp"
-#include "rtc_jit_sources.inc"  // kSrcKernels, kSrcInternal, kSrcRtcH (tools/embed_sources.py)
+#include "rtc_jit_cache.hpp"
+#include "rtc_jit_sources.inc"  // kSrcKernels, kSrcInternal, kSrcRtcH, kBuildExtra (tools/embed_sources.py)
+
+extern char** environ;
 
 namespace rtc {
+
+// One per-scene kernel build: the code object of (world table, variant),
+// compiled by a child process and shared by every context of the process
+// that uploads the same world.
+struct CodeBuild {
+    std::atomic<int> state{0};  // 0 compiling, 1 ready, 2 failed
+    jitfile::CodeObject co;
+    std::string log;
+    double ms = 0;              // compile (child process wall time) or disk-cache load
+    bool from_disk = false;
+};
+
 namespace {
+
+using jitfile::fnv;
 
 std::string hexf(float v) {
     uint32_t b;
@@ -82,117 +107,26 @@ std::string scene_header(const std::vector<ShapeRec<float>>& sh, const int32_t b
     return s;
 }
 
-uint64_t fnv(const void* p, size_t n, uint64_t h = 1469598103934665603ull) {
-    const unsigned char* b = static_cast<const unsigned char*>(p);
-    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
-    return h;
-}
-
 const char* kernel_name(bool pool, bool lds) {
     if (pool) return lds ? "rtc::trace_pool<float, true, false>" : "rtc::trace_pool<float, false, false>";
     return lds ? "rtc::trace_direct<float, true>" : "rtc::trace_direct<float, false>";
 }
 
-struct CodeObject {
-    std::vector<char> code;
-    std::string lowered;
-    double compile_ms = 0;
-    bool from_disk = false;
-    uint64_t key = 0;  // the disk cache key (every input of the compile)
-};
-
-}  // namespace
-
-// One per-scene kernel build: the code object of (world table, variant),
-// compiled on a host thread (or in line for RT_JIT_SYNC) and shared by every
-// context of the process that uploads the same world.
-struct CodeBuild {
-    std::atomic<int> state{0};  // 0 compiling, 1 ready, 2 failed
-    CodeObject co;
-    std::string log;
-};
-
-namespace {
-
-// ------------------------------------------------------- on-disk code cache
-// One file per build: "RTCJIT2\n" <lowered name> "\n" <code bytes> " "
-// <FNV-1a of the code, hex> "\n" <code object>, named by a 64-bit FNV-1a of
-// every input of the compile.  Written to a temporary name and renamed, so
-// concurrent processes never read a partial file; a file whose length or
-// checksum does not match is ignored and rebuilt (a damaged code object
-// handed to hipModuleLoadData can abort the process instead of failing).
-constexpr char kCacheMagic[] = "RTCJIT2\n";
-
-std::string cache_dir() {
-    const char* e = std::getenv("RTC_JIT_CACHE");
-    if (e) return (!*e || !std::strcmp(e, "0")) ? std::string() : std::string(e);
-    if (const char* x = std::getenv("XDG_CACHE_HOME"); x && *x) return std::string(x) + "/rtc_jit";
-    if (const char* h = std::getenv("HOME"); h && *h) return std::string(h) + "/.cache/rtc_jit";
-    return std::string();
-}
-
-bool make_dirs(const std::string& d) {
-    for (size_t p = 1; p <= d.size(); ++p) {
-        if (p < d.size() && d[p] != '/') continue;
-        const std::string part = d.substr(0, p);
-        if (::mkdir(part.c_str(), 0755) != 0 && errno != EEXIST) return false;
-    }
-    return true;
-}
-
-std::string cache_path(const std::string& dir, uint64_t key) {
-    char buf[32];
-    std::snprintf(buf, sizeof buf, "/%016llx.co", (unsigned long long)key);
-    return dir + buf;
-}
-
-bool cache_load(const std::string& path, CodeObject& out) {
-    FILE* f = std::fopen(path.c_str(), "rb");
-    if (!f) return false;
-    std::vector<char> all;
-    char buf[1 << 16];
-    for (size_t n; (n = std::fread(buf, 1, sizeof buf, f)) > 0;) all.insert(all.end(), buf, buf + n);
-    std::fclose(f);
-    const size_t m = sizeof kCacheMagic - 1;
-    if (all.size() < m || std::memcmp(all.data(), kCacheMagic, m)) return false;
-    size_t nl = m;
-    while (nl < all.size() && all[nl] != '\n') ++nl;
-    if (nl + 1 >= all.size() || nl == m) return false;
-    size_t nl2 = nl + 1;
-    while (nl2 < all.size() && all[nl2] != '\n') ++nl2;
-    if (nl2 >= all.size()) return false;
-    unsigned long long len = 0, sum = 0;
-    const std::string meta(all.data() + nl + 1, nl2 - nl - 1);
-    if (std::sscanf(meta.c_str(), "%llu %llx", &len, &sum) != 2) return false;
-    if (len == 0 || all.size() - (nl2 + 1) != len || fnv(all.data() + nl2 + 1, len) != sum) return false;
-    out.lowered.assign(all.data() + m, nl - m);
-    out.code.assign(all.begin() + (ptrdiff_t)(nl2 + 1), all.end());
-    out.from_disk = true;
-    return true;
-}
-
-void cache_store(const std::string& dir, const std::string& path, const CodeObject& co) {
-    if (!make_dirs(dir)) return;
-    static std::atomic<unsigned> seq{0};  // contexts of one process may build the same key at once
-    const std::string tmp = path + ".tmp" + std::to_string((long long)::getpid()) + "." + std::to_string(seq++);
-    FILE* f = std::fopen(tmp.c_str(), "wb");
-    if (!f) return;
-    bool ok = std::fwrite(kCacheMagic, 1, sizeof kCacheMagic - 1, f) == sizeof kCacheMagic - 1;
-    ok = ok && std::fwrite(co.lowered.data(), 1, co.lowered.size(), f) == co.lowered.size();
-    ok = ok && std::fprintf(f, "\n%llu %llx\n", (unsigned long long)co.code.size(),
-                            (unsigned long long)fnv(co.code.data(), co.code.size())) > 0;
-    ok = ok && std::fwrite(co.code.data(), 1, co.code.size(), f) == co.code.size();
-    ok = (std::fclose(f) == 0) && ok;
-    if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
-}
-
-// Identity of a shared object: path, size and modification time.
+// Identity of a file: path, size and modification time.
 uint64_t file_identity(const char* path, uint64_t h) {
     struct stat st;
     if (!path || ::stat(path, &st) != 0) return fnv("?", 1, h);
     h = fnv(path, std::strlen(path) + 1, h);
     const int64_t v[2] = {(int64_t)st.st_size, (int64_t)st.st_mtime};
     return fnv(v, sizeof v, h);
+}
+
+std::string librtc_dir() {
+    Dl_info self{};
+    if (!dladdr(reinterpret_cast<void*>(&scene_header), &self) || !self.dli_fname) return ".";
+    std::string p(self.dli_fname);
+    const size_t slash = p.find_last_of('/');
+    return slash == std::string::npos ? "." : p.substr(0, slash);
 }
 
 // The toolchain and library behind a build, for the disk cache key: hipRTC
@@ -209,7 +143,7 @@ uint64_t toolchain_identity() {
         (void)hipDriverGetVersion(&v[3]);
         h = fnv(v, sizeof v, h);
         Dl_info self{}, rtcc{};
-        if (dladdr(reinterpret_cast<void*>(&toolchain_identity), &self)) h = file_identity(self.dli_fname, h);
+        if (dladdr(reinterpret_cast<void*>(&scene_header), &self)) h = file_identity(self.dli_fname, h);
         if (dladdr(reinterpret_cast<void*>(&hiprtcCompileProgram), &rtcc) && rtcc.dli_fname) {
             h = file_identity(rtcc.dli_fname, h);
             std::string dir(rtcc.dli_fname);
@@ -228,27 +162,6 @@ uint64_t toolchain_identity() {
     return id;
 }
 
-// Process-wide caches: builds by (table, kernel variant); loaded functions
-// by (build, device).  Build threads are joined when librtc is unloaded (the
-// registry is declared last, so it is destroyed first).
-std::mutex g_mu;
-std::condition_variable g_cv;  // a build finished
-std::map<std::pair<uint64_t, int>, std::shared_ptr<CodeBuild>> g_code;
-std::map<std::pair<uint64_t, int>, std::pair<hipModule_t, hipFunction_t>> g_fn;
-struct BuildThreads {
-    std::mutex mu;
-    std::vector<std::thread> threads;
-    ~BuildThreads() {
-        std::lock_guard<std::mutex> lk(mu);
-        for (std::thread& t : threads)
-            if (t.joinable()) t.join();
-    }
-    void add(std::thread t) {
-        std::lock_guard<std::mutex> lk(mu);
-        threads.push_back(std::move(t));
-    }
-} g_threads;
-
 // The static build's EXTRA flags (Makefile), passed on to hipRTC: -D/-U only.
 std::vector<std::string> build_defines() {
     std::vector<std::string> out;
@@ -263,120 +176,182 @@ std::vector<std::string> build_defines() {
     return out;
 }
 
-int compile(const std::string& scene, const char* name, const std::string& arch, CodeObject& out, std::string& log,
-            bool use_cache = true) {
-    const std::string main_src = std::string("#define RTC_JIT 1\n#include \"rtc_jit_scene.hpp\"\n") + kSrcKernels;
-    const char* headers[] = {scene.c_str(), kSrcInternal, kSrcRtcH};
-    const char* names[] = {"rtc_jit_scene.hpp", "rtc_internal.hpp", "../../include/rtc.h"};
-    hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, main_src.c_str(), "rtc_kernels_scene.hip", 3, headers, names) != HIPRTC_SUCCESS)
-        return set_error(RT_ERR_HIP, "hiprtcCreateProgram failed");
-    hiprtcAddNameExpression(prog, name);
+// Everything the compiler sees for one build, and the key naming it.
+jitfile::Request make_request(const std::string& scene, const char* name, const std::string& arch, uint64_t* key) {
+    jitfile::Request rq;
+    rq.name = name;
+    rq.main_src = std::string("#define RTC_JIT 1\n#include \"rtc_jit_scene.hpp\"\n") + kSrcKernels;
+    rq.headers = {{"rtc_jit_scene.hpp", scene}, {"rtc_internal.hpp", kSrcInternal}, {"../../include/rtc.h", kSrcRtcH}};
     // The flags of the static build (Makefile): no contraction beyond the
     // source's explicit fmas, no SLP packing.  Plus no machine-level LICM:
     // with the records as constants it hoists their materialisations (and
     // values computed from them) out of the generation and tile loops, where
     // they are held across the loop and spill (reflect_refract's pool kernel:
     // 100 B/lane of scratch and 106 SGPRs with it, 8 B and 73 VGPRs without).
-    // The device's own gfx target.  A build with defines of its own
-    // (Makefile EXTRA: tuning macros, f32 math variants) passes all of them
-    // on, so both builds run the same arithmetic and plan the same occupancy.
-    const std::string arch_opt = "--offload-arch=" + arch;
-    std::vector<const char*> opts = {arch_opt.c_str(),     "-O3",    "-std=c++20", "-ffp-contract=off",
-                                     "-fno-slp-vectorize", "-mllvm", "-disable-machine-licm"};
+    // The device's own gfx target.  A build with defines of its own (Makefile
+    // EXTRA: tuning macros, f32 math variants) passes all of them on, so both
+    // builds run the same arithmetic and plan the same occupancy.
+    rq.opts = {"--offload-arch=" + arch, "-O3", "-std=c++20", "-ffp-contract=off", "-fno-slp-vectorize", "-mllvm",
+               "-disable-machine-licm"};
     static const std::vector<std::string> defines = build_defines();
-    for (const std::string& d : defines) opts.push_back(d.c_str());
+    rq.opts.insert(rq.opts.end(), defines.begin(), defines.end());
     // The direct kernel fences the ray at every third shape only: the shape
     // tests in between may interleave (more ILP) and still fit 8 waves/SIMD
     // without spilling.  Same-box A/B against a fence per shape: shadow_puppets
     // -3.6 %, three_sphere 4K -2.5 %, 1080p -0.6 %; the pool kernel lost 15 %
     // on cover that way and keeps a fence per shape.
-    if (!std::strstr(name, "pool")) opts.push_back("-DRTC_JIT_FENCE_EVERY=3");
+    if (!std::strstr(name, "pool")) rq.opts.push_back("-DRTC_JIT_FENCE_EVERY=3");
     // RTC_JIT_FLAGS: extra compiler options, space-separated (A/B diagnostics)
-    std::vector<std::string> extra;
     if (const char* e = std::getenv("RTC_JIT_FLAGS")) {
-        std::string all(e);
+        const std::string all(e);
         for (size_t p = 0; p < all.size();) {
             size_t q = all.find(' ', p);
             if (q == std::string::npos) q = all.size();
-            if (q > p) extra.push_back(all.substr(p, q - p));
+            if (q > p) rq.opts.push_back(all.substr(p, q - p));
             p = q + 1;
         }
     }
-    for (const std::string& x : extra) opts.push_back(x.c_str());
-    // the disk cache key: every input of the compile, and the toolchain
-    uint64_t key = fnv(main_src.data(), main_src.size());
-    for (const char* h : headers) key = fnv(h, std::strlen(h) + 1, key);
-    for (const char* o : opts) key = fnv(o, std::strlen(o) + 1, key);
-    key = fnv(name, std::strlen(name) + 1, key);
+    uint64_t k = fnv(rq.main_src.data(), rq.main_src.size());
+    for (const auto& h : rq.headers) k = fnv(h.second.data(), h.second.size() + 1, fnv(h.first.data(), h.first.size() + 1, k));
+    for (const std::string& o : rq.opts) k = fnv(o.data(), o.size() + 1, k);
+    k = fnv(rq.name.data(), rq.name.size() + 1, k);
     const uint64_t tool = toolchain_identity();
-    key = fnv(&tool, sizeof tool, key);
-    out.key = key;
-    const std::string dir = cache_dir();
-    const std::string path = dir.empty() || !use_cache ? std::string() : cache_path(dir, key);
-    if (!path.empty()) {
-        const auto c0 = std::chrono::steady_clock::now();
-        if (cache_load(path, out)) {
-            hiprtcDestroyProgram(&prog);
-            out.compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
-            return RT_OK;
-        }
-    }
-    const auto t0 = std::chrono::steady_clock::now();
-    const hiprtcResult r = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
-    out.compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    size_t n = 0;
-    hiprtcGetProgramLogSize(prog, &n);
-    log.assign(n, '\0');
-    if (n) hiprtcGetProgramLog(prog, &log[0]);
-    int rc = RT_OK;
-    if (r != HIPRTC_SUCCESS) {
-        rc = set_error(RT_ERR_HIP, std::string("hiprtcCompileProgram: ") + hiprtcGetErrorString(r) + "\n" + log);
-    } else {
-        const char* lowered = nullptr;
-        hiprtcGetLoweredName(prog, name, &lowered);
-        out.lowered = lowered ? lowered : "";
-        size_t cs = 0;
-        hiprtcGetCodeSize(prog, &cs);
-        out.code.resize(cs);
-        hiprtcGetCode(prog, out.code.data());
-        if (out.lowered.empty() || cs == 0) rc = set_error(RT_ERR_HIP, "hipRTC produced no kernel");
-        else if (!path.empty()) cache_store(dir, path, out);
-        if (const char* dir = std::getenv("RTC_JIT_DUMP")) {  // diagnostics: scene header + code object
-            const std::string base = std::string(dir) + "/" + std::to_string(fnv(scene.data(), scene.size())) + "_" +
-                                     (std::strstr(name, "pool") ? "pool" : "direct");
-            if (FILE* f = std::fopen((base + ".hpp").c_str(), "w")) {
-                std::fwrite(scene.data(), 1, scene.size(), f);
-                std::fclose(f);
-            }
-            if (FILE* f = std::fopen((base + ".co").c_str(), "wb")) {
-                std::fwrite(out.code.data(), 1, out.code.size(), f);
-                std::fclose(f);
-            }
-        }
-    }
-    hiprtcDestroyProgram(&prog);
-    return rc;
+    *key = fnv(&tool, sizeof tool, k);
+    return rq;
 }
 
-// Compile one build (host thread or in line) and publish it.
-void run_build(std::shared_ptr<CodeBuild> b, std::string scene, std::string name, std::string arch) {
-    std::string log;
-    const int rc = compile(scene, name.c_str(), arch, b->co, log);
+std::string cache_dir() {
+    const char* e = std::getenv("RTC_JIT_CACHE");
+    if (e) return (!*e || !std::strcmp(e, "0")) ? std::string() : std::string(e);
+    if (const char* x = std::getenv("XDG_CACHE_HOME"); x && *x) return std::string(x) + "/rtc_jit";
+    if (const char* h = std::getenv("HOME"); h && *h) return std::string(h) + "/.cache/rtc_jit";
+    return std::string();
+}
+
+std::string cache_path(const std::string& dir, uint64_t key) {
+    char buf[32];
+    std::snprintf(buf, sizeof buf, "/%016llx.co", (unsigned long long)key);
+    return dir + buf;
+}
+
+std::string temp_path(const char* suffix) {
+    static std::atomic<unsigned> seq{0};
+    const char* t = std::getenv("TMPDIR");
+    return std::string(t && *t ? t : "/tmp") + "/rtcjit-" + std::to_string((long long)::getpid()) + "-" +
+           std::to_string(seq++) + suffix;
+}
+
+// Process-wide state, never destroyed: build waiters are detached threads
+// and may still run while the process exits.
+std::mutex& g_mu = *new std::mutex;
+std::condition_variable& g_cv = *new std::condition_variable;  // a build finished
+auto& g_code = *new std::map<std::pair<uint64_t, int>, std::shared_ptr<CodeBuild>>;   // (table, variant)
+auto& g_fn = *new std::map<std::pair<uint64_t, int>, std::pair<hipModule_t, hipFunction_t>>;  // (build, device)
+
+void finish(const std::shared_ptr<CodeBuild>& b, bool ok, std::string log) {
     {
         std::lock_guard<std::mutex> lk(g_mu);
-        if (rc) b->log = std::string(rt_last_error());
-        b->state.store(rc ? 2 : 1, std::memory_order_release);
+        b->log = std::move(log);
+        b->state.store(ok ? 1 : 2, std::memory_order_release);
     }
     g_cv.notify_all();
+}
+
+// Wait for the compiler process (its output through `fd` until EOF, then its
+// status), load what it wrote to `out`, publish the build.
+void await_child(std::shared_ptr<CodeBuild> b, pid_t pid, int fd, std::string out, bool temp_out,
+                 std::chrono::steady_clock::time_point t0) {
+    std::string log;
+    char buf[4096];
+    for (;;) {
+        const ssize_t n = ::read(fd, buf, sizeof buf);
+        if (n > 0) {
+            if (log.size() < (1u << 20)) log.append(buf, (size_t)n);
+        } else if (n < 0 && errno == EINTR) {
+            continue;
+        } else {
+            break;
+        }
+    }
+    ::close(fd);
+    int status = 0;
+    pid_t w;
+    do {
+        w = ::waitpid(pid, &status, 0);
+    } while (w < 0 && errno == EINTR);
+    // a host that reaps children itself (SIGCHLD ignored): judge by the output
+    const bool exited_ok = w < 0 ? true : (WIFEXITED(status) && WEXITSTATUS(status) == 0);
+    const bool ok = exited_ok && jitfile::read_code(out, b->co);
+    if (temp_out) std::remove(out.c_str());
+    b->ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (!ok && log.empty()) log = "rtc_jitc failed (status " + std::to_string(status) + ")";
+    finish(b, ok, ok ? std::string() : "per-scene build failed: " + log);
+}
+
+// Start one build: from the disk cache at once, or by a compiler process
+// (waited for in line when `sync`, else by a detached thread).
+void start_build(const std::shared_ptr<CodeBuild>& b, const jitfile::Request& rq, uint64_t key, bool sync) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const std::string dir = cache_dir();
+    const std::string path = dir.empty() ? std::string() : cache_path(dir, key);
+    if (!path.empty() && jitfile::read_code(path, b->co)) {
+        b->from_disk = true;
+        b->ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        finish(b, true, std::string());
+        return;
+    }
+    const char* env_helper = std::getenv("RTC_JITC");
+    const std::string helper = env_helper && *env_helper ? env_helper : librtc_dir() + "/rtc_jitc";
+    if (::access(helper.c_str(), X_OK) != 0) {
+        finish(b, false, "per-scene build: compiler " + helper + " not found (the generic kernel is used)");
+        return;
+    }
+    const std::string req = temp_path(".req");
+    const bool temp_out = path.empty();
+    const std::string out = temp_out ? temp_path(".co") : path;
+    if (!jitfile::write_request(req, rq)) {
+        finish(b, false, "per-scene build: cannot write " + req);
+        return;
+    }
+    int fds[2];
+    if (::pipe2(fds, O_CLOEXEC) != 0) {
+        std::remove(req.c_str());
+        finish(b, false, std::string("per-scene build: pipe: ") + std::strerror(errno));
+        return;
+    }
+    posix_spawn_file_actions_t fa;
+    posix_spawn_file_actions_init(&fa);
+    posix_spawn_file_actions_adddup2(&fa, fds[1], 1);
+    posix_spawn_file_actions_adddup2(&fa, fds[1], 2);
+    std::vector<char*> argv = {const_cast<char*>(helper.c_str()), const_cast<char*>(req.c_str()),
+                               const_cast<char*>(out.c_str()), nullptr};
+    pid_t pid = 0;
+    const int e = posix_spawn(&pid, helper.c_str(), &fa, nullptr, argv.data(), environ);
+    posix_spawn_file_actions_destroy(&fa);
+    ::close(fds[1]);
+    if (e != 0) {
+        ::close(fds[0]);
+        std::remove(req.c_str());
+        finish(b, false, std::string("per-scene build: cannot start ") + helper + ": " + std::strerror(e));
+        return;
+    }
+    if (sync) {
+        await_child(b, pid, fds[0], out, temp_out, t0);
+        return;
+    }
+    try {
+        std::thread(await_child, b, pid, fds[0], out, temp_out, t0).detach();
+    } catch (const std::exception&) {  // no thread: wait in line instead
+        await_child(b, pid, fds[0], out, temp_out, t0);
+    }
 }
 
 }  // namespace
 
 // The per-scene kernel for this context's uploaded world, or null (use the
-// generic kernel this launch).  RT_JIT_SYNC compiles in line; RT_JIT_AUTO /
-// RT_JIT_EAGER start the compile on a host thread at the 2nd / 1st large
-// frame of an upload and return null until it has landed.
+// generic kernel this launch).  RT_JIT_SYNC builds in line; RT_JIT_AUTO /
+// RT_JIT_EAGER start the build at the 2nd / 1st large frame of an upload and
+// return null until it has landed.
 int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int static_blocks, hipFunction_t* fn) {
     *fn = nullptr;
     if (ctx->jit_failed || ctx->jit_shapes.empty()) return RT_OK;
@@ -386,49 +361,42 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
         return RT_OK;
     }
     if (ctx->jit_rejected[variant]) return RT_OK;
+    const bool sync = ctx->jit_mode == RT_JIT_SYNC;
     std::shared_ptr<CodeBuild>& b = ctx->jit_build[variant];
     if (!b) {
-        const uint64_t key = fnv(ctx->jit_begin, sizeof ctx->jit_begin,
-                                 fnv(ctx->jit_shapes.data(), ctx->jit_shapes.size() * sizeof(ShapeRec<float>)));
-        const bool sync = ctx->jit_mode == RT_JIT_SYNC;
+        const uint64_t table = fnv(ctx->jit_begin, sizeof ctx->jit_begin,
+                                   fnv(ctx->jit_shapes.data(), ctx->jit_shapes.size() * sizeof(ShapeRec<float>)));
         const uint32_t start_at = ctx->jit_mode == RT_JIT_AUTO ? 2 : 1;
         bool start = false;
         {
             std::lock_guard<std::mutex> lk(g_mu);
-            auto it = g_code.find({key, variant});
+            auto it = g_code.find({table, variant});
             if (it != g_code.end()) {
                 b = it->second;  // built (or building, or failed) for another context or an earlier upload
             } else if (sync || ctx->jit_frames >= start_at) {
                 b = std::make_shared<CodeBuild>();
-                g_code[{key, variant}] = b;
+                g_code[{table, variant}] = b;
                 start = true;
             }
         }
         if (!b) return RT_OK;
         if (start) {
             ctx->jit_owner[variant] = true;
-            std::string scene = scene_header(ctx->jit_shapes, ctx->jit_begin);
-            if (sync) {
-                run_build(b, std::move(scene), kernel_name(pool, lds), ctx->arch);
-            } else {
-                try {
-                    g_threads.add(std::thread(run_build, b, std::move(scene), std::string(kernel_name(pool, lds)),
-                                              ctx->arch));
-                } catch (const std::exception& e) {  // no thread: build in line instead
-                    run_build(b, scene_header(ctx->jit_shapes, ctx->jit_begin), kernel_name(pool, lds), ctx->arch);
-                }
-            }
+            uint64_t key = 0;
+            const jitfile::Request rq =
+                make_request(scene_header(ctx->jit_shapes, ctx->jit_begin), kernel_name(pool, lds), ctx->arch, &key);
+            start_build(b, rq, key, sync);
         }
     }
-    if (ctx->jit_mode == RT_JIT_SYNC) {  // wait for a build another context started
+    if (sync) {  // a build another context started: wait for it
         std::unique_lock<std::mutex> lk(g_mu);
         g_cv.wait(lk, [&] { return b->state.load() != 0; });
     }
     const int state = b->state.load(std::memory_order_acquire);
     if (state == 0) return RT_OK;  // still compiling: the generic kernel this frame
     if (ctx->jit_owner[variant]) {
-        ctx->jit_compile_ms += b->co.compile_ms;
-        if (b->co.from_disk) ++ctx->jit_cache_hits;
+        ctx->jit_compile_ms += b->ms;
+        if (b->from_disk) ++ctx->jit_cache_hits;
         ctx->jit_owner[variant] = false;
     }
     if (state == 2) {
@@ -492,7 +460,7 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
 // Block until this context's builds in flight have finished (rt_jit_wait).
 int jit_wait(rt_context* ctx, double timeout_ms, int* pending) {
     const auto deadline = std::chrono::steady_clock::now() +
-                          std::chrono::microseconds((int64_t)(timeout_ms < 0 ? 3.6e9 * 1e3 : timeout_ms * 1e3));
+                          std::chrono::microseconds((int64_t)(timeout_ms < 0 ? 3.6e12 : timeout_ms * 1e3));
     auto left = [ctx] {
         int n = 0;
         for (const auto& b : ctx->jit_build) n += b && b->state.load() == 0;

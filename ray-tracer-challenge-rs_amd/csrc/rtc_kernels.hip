@@ -8,8 +8,9 @@
 //    spawn a child (no material with reflectiveness/transparency != 0, or
 //    max_depth == 0): the whole per-pixel tree is one shaded hit plus L shadow
 //    rays.  This is three_sphere_scene, the BASELINE metric's config.
-//  * trace_pool    — wavefront tracer.  A workgroup owns a 16x16 tile; the
-//    tile's rays live in LDS (SoA) as a LIFO pool.  Each iteration pops up to
+//  * trace_pool    — wavefront tracer.  A workgroup owns a 64x4 tile
+//    (RT_TILE_W x RT_TILE_H, each wave a 16x4 block of it); the tile's rays
+//    live in LDS (SoA) as a LIFO pool.  Each iteration pops up to
 //    `pop_batch` rays, traces them one per lane (closest hit, shading, any-hit
 //    shadow rays), accumulates weight x surface colour into the tile's pixel
 //    accumulators, and pushes the reflection/refraction children, compacted
@@ -18,8 +19,10 @@
 //    The recursion is linear in scalar weights (world.rs:54-66, 127, 156), so
 //    pixel = sum over tree nodes of (product of weights) x surface colour.
 //
-// Tiles are handed out by a cumulative atomic counter (dynamic load balance
-// over a grid sized to the resident workgroup count).  World tables are read
+// Pool tiles are handed out by 8 per-XCD atomic queues with stealing
+// (dynamic load balance over a grid sized to the resident workgroup count),
+// heaviest first once a launch has recorded the tiles' costs; direct tiles by
+// a static stride over 2.5x the resident grid.  World tables are read
 // with wave-uniform scalar loads in per-type loops (rtc_internal.hpp).
 //
 // Two instantiations: R = float (the throughput path) and R = double (parity:

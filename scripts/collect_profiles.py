@@ -34,6 +34,21 @@ def pmc_means(d, pat="trace_"):
     return {k: sum(v) / len(v) for k, v in sorted(agg.items())}
 
 
+def kernel_medians(d):
+    """Per-kernel median, mean and count of the dispatch durations (us) in a
+    kernel trace: ramp outliers (first launches at low clocks) pull the
+    stats CSV's mean above the steady per-launch time."""
+    durs = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            durs[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3)
+    out = {}
+    for k, v in durs.items():
+        v.sort()
+        out[k] = {"calls": len(v), "median_us": v[len(v) // 2], "mean_us": sum(v) / len(v), "max_us": v[-1]}
+    return out
+
+
 def main():
     rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
     out = os.path.join(ROOT, "profiles")
@@ -44,6 +59,9 @@ def main():
         src = os.path.join(ROOT, "gpurun_out", f"{rnd}_stats_{key}")
         for f in glob.glob(os.path.join(src, "**", "*kernel_stats.csv"), recursive=True):
             shutil.copy(f, os.path.join(out, f"{rnd}_kernel_stats_{key}.csv"))
+        med = kernel_medians(src)
+        if med:
+            json.dump(med, open(os.path.join(out, f"{rnd}_kernel_medians_{key}.json"), "w"), indent=1)
         log = os.path.join(src, "bench.log")
         if os.path.exists(log):
             lines = [l for l in open(log) if l.startswith("{")]

@@ -168,6 +168,53 @@ def test_destroy_with_a_build_in_flight(rtc):
         assert c2.jit_status()["used"] and np.array_equal(a, b)
 
 
+_EXIT_PROBE = r"""
+import json, os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "ray-tracer-challenge-rs_amd"))
+import rtc_amd
+from rtc_amd import scene_io
+scene = scene_io.load(os.path.join(sys.argv[1], "tests", "golden", "scenes", "cover.json"))
+cam = rtc_amd.camera_resize(scene.camera, 640, 360)
+ctx = rtc_amd.Context(0)
+ctx.set_jit(int(sys.argv[2]))
+ctx.upload(scene)
+img, st = ctx.render(cam, 6, precision="f32")
+js = ctx.jit_status()
+print(json.dumps({"used": js["used"], "ms": js["compile_ms"], "rays": st["rays"]}), flush=True)
+"""  # exits with the per-scene build (when started) still compiling
+
+
+def test_exit_with_a_build_in_flight(tmp_path):
+    """A host that exits while its per-scene build compiles exits cleanly (the
+    compile runs in a child process, csrc/rtc_jitc.cpp; on a thread it had
+    corrupted the heap at exit), and the build still lands in the disk cache
+    for the next process."""
+    import json
+    import os
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cache = tmp_path / "cache"
+    env = dict(os.environ, RTC_JIT_CACHE=str(cache))
+
+    def run(mode):
+        out = subprocess.run([sys.executable, "-c", _EXIT_PROBE, root, str(mode)], env=env, capture_output=True,
+                             text=True, timeout=100)
+        assert out.returncode == 0, out.stderr[-2000:]
+        return json.loads(out.stdout.strip().splitlines()[-1])
+
+    first = run(3)  # RT_JIT_EAGER: the build starts at this frame, the process exits at once
+    assert not first["used"]
+    deadline = time.time() + 60
+    while time.time() < deadline and not (cache.exists() and any(p.suffix == ".co" for p in cache.iterdir())):
+        time.sleep(0.2)
+    assert any(p.suffix == ".co" for p in cache.iterdir()), "the orphaned compile did not land in the cache"
+    second = run(3)  # the build comes from the disk cache at the first frame
+    assert second["used"] and second["rays"] == first["rays"]
+    assert second["ms"] < 100, second
+
+
 def test_failed_launch_keeps_the_queue_heads(gpu_ctx, rtc):
     """A pool launch that fails after planning (RT_FLAG_FAIL_LAUNCH) must not
     consume a set of queue heads: the next frame is complete and equal."""
@@ -211,7 +258,9 @@ def test_per_scene_build_disk_cache(tmp_path):
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, RTC_JIT_CACHE=str(tmp_path / "cache"))
+    # comgr keeps a compile cache of its own (on by default): a fresh one, so
+    # the first process really compiles
+    env = dict(os.environ, RTC_JIT_CACHE=str(tmp_path / "cache"), AMD_COMGR_CACHE_DIR=str(tmp_path / "comgr"))
 
     def run():
         out = subprocess.run([sys.executable, "-c", _CACHE_PROBE, root], env=env, capture_output=True, text=True,
