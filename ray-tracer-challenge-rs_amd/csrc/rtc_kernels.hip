@@ -1277,15 +1277,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
 // Ray pool: a LIFO of pending rays per workgroup.  Slots [0, lds_cap) live
 // in dynamic LDS after the world tables:
 //   [acc: 3 x kBlock i64][ox oy oz dx dy dz w : lds_cap x R][meta : lds_cap x u32]
-// and slots [lds_cap, cap) in this workgroup's region of P.spill (same SoA
-// layout, cap - lds_cap entries per array).  The LIFO bound cap = P + depth x
+// and slots [lds_cap, cap) in this workgroup's region of P.spill, one 8-word
+// record per entry (AoS: a lane's entry is two dwordx4 stores / loads in f32,
+// where the SoA layout took eight dword instructions per entry).  The LIFO bound cap = P + depth x
 // batch is what makes overflow impossible; the LDS part is sized for
 // occupancy (rtc_host.cpp plan_launch), the rare deep excursions spill.
 template <typename R>
 struct Pool {
     long long* acc;
     R* lds;    // 8 arrays of lds_cap words: ox oy oz dx dy dz w, then meta (u32)
-    R* spill;  // 8 arrays of spill_cap words (this workgroup's region)
+    R* spill;  // spill_cap records of 8 words (this workgroup's region)
     int lds_cap, spill_cap;
 };
 
@@ -1329,15 +1330,53 @@ __device__ inline void pool_load(PR base, PU metas, int n, int i, V3<R>& o, V3<R
     meta = metas[i];
 }
 
+// A spilled entry: {o.x, o.y, o.z, d.x} {d.y, d.z, w, meta bits} (f32: two
+// 16-byte vector accesses; f64: four).  The meta word travels as raw bits.
+template <typename R>
+__device__ inline void spill_store(RTC_AS_GLOBAL R* e, V3<R> o, V3<R> d, R w, uint32_t meta) {
+    if constexpr (sizeof(R) == 4) {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        RTC_AS_GLOBAL f4* p = (RTC_AS_GLOBAL f4*)e;
+        p[0] = f4{o.x, o.y, o.z, d.x};
+        p[1] = f4{d.y, d.z, w, __uint_as_float(meta)};
+    } else {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        RTC_AS_GLOBAL d2* p = (RTC_AS_GLOBAL d2*)e;
+        p[0] = d2{o.x, o.y};
+        p[1] = d2{o.z, d.x};
+        p[2] = d2{d.y, d.z};
+        p[3] = d2{w, __longlong_as_double((long long)meta)};
+    }
+}
+
+template <typename R>
+__device__ inline void spill_load(const RTC_AS_GLOBAL R* e, V3<R>& o, V3<R>& d, R& w, uint32_t& meta) {
+    if constexpr (sizeof(R) == 4) {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const RTC_AS_GLOBAL f4* p = (const RTC_AS_GLOBAL f4*)e;
+        const f4 a = p[0], b = p[1];
+        o = {a.x, a.y, a.z};
+        d = {a.w, b.x, b.y};
+        w = b.z;
+        meta = __float_as_uint(b.w);
+    } else {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        const RTC_AS_GLOBAL d2* p = (const RTC_AS_GLOBAL d2*)e;
+        const d2 a = p[0], b = p[1], c = p[2], q = p[3];
+        o = {a.x, a.y, b.x};
+        d = {b.y, c.x, c.y};
+        w = q.x;
+        meta = (uint32_t)__double_as_longlong(q.y);
+    }
+}
+
 template <typename R>
 __device__ inline void pool_put(const Pool<R>& pl, int slot, V3<R> o, V3<R> d, R w, uint32_t meta) {
     if (slot < pl.lds_cap) {
         RTC_AS_LDS R* b = (RTC_AS_LDS R*)pl.lds;
         pool_store<R>(b, (RTC_AS_LDS uint32_t*)(b + 7 * pl.lds_cap), pl.lds_cap, slot, o, d, w, meta);
     } else {
-        RTC_AS_GLOBAL R* b = (RTC_AS_GLOBAL R*)pl.spill;
-        pool_store<R>(b, (RTC_AS_GLOBAL uint32_t*)(b + 7 * pl.spill_cap), pl.spill_cap, slot - pl.lds_cap, o, d,
-                      w, meta);
+        spill_store<R>((RTC_AS_GLOBAL R*)pl.spill + 8 * (size_t)(slot - pl.lds_cap), o, d, w, meta);
     }
 }
 
@@ -1347,9 +1386,7 @@ __device__ inline void pool_get(const Pool<R>& pl, int slot, V3<R>& o, V3<R>& d,
         const RTC_AS_LDS R* b = (const RTC_AS_LDS R*)pl.lds;
         pool_load<R>(b, (const RTC_AS_LDS uint32_t*)(b + 7 * pl.lds_cap), pl.lds_cap, slot, o, d, w, meta);
     } else {
-        const RTC_AS_GLOBAL R* b = (const RTC_AS_GLOBAL R*)pl.spill;
-        pool_load<R>(b, (const RTC_AS_GLOBAL uint32_t*)(b + 7 * pl.spill_cap), pl.spill_cap, slot - pl.lds_cap, o, d,
-                     w, meta);
+        spill_load<R>((const RTC_AS_GLOBAL R*)pl.spill + 8 * (size_t)(slot - pl.lds_cap), o, d, w, meta);
     }
 }
 

@@ -13,12 +13,13 @@ import rtc_amd  # noqa: E402
 from rtc_amd import scene_io  # noqa: E402
 
 name, w, h = (sys.argv[1], int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else ("cover", 3840, 2160)
+COUNTS = [int(x) for x in os.environ.get("SHARD_COUNTS", "1,2,4,8").split(",")]
 scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{name}.json"))
 cam = rtc_amd.camera_resize(scene.camera, w, h)
 s = torch.cuda.current_stream()
 with rtc_amd.Context(0) as ctx:
     ctx.upload(scene)
-    for shards in (1, 2, 4, 8):
+    for shards in COUNTS:
         rows = rtc_amd.shard_rows(h, shards)
         out = torch.empty((rows, w, 3), dtype=torch.uint8, device="cuda")
         times = []
