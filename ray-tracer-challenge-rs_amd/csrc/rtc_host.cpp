@@ -557,7 +557,10 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     // previous user of that set is complete by stream order).
     // The set flips only once the launch is enqueued: a launch that fails
     // before that leaves its set unused and still zero for the next one.
-    const bool dynamic = ls.sched == kSchedDynamic;
+    // (pool launches only: the direct kernel reads no queue heads and zeroes
+    // none, so a dynamic direct launch (RTC_SCHED_DIRECT=dynamic) must not
+    // flip the sets under the next pool launch)
+    const bool dynamic = ls.pool && ls.sched == kSchedDynamic;
     if (dynamic) {
         const size_t set = (size_t)kTileQueues * kQueueStride;
         P.tile_counter = ctx->d_tile_counter + (ctx->head_set ? set : 0);

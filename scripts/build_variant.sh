@@ -10,7 +10,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 T=$(mktemp -d /tmp/rtc_variant_XXXX)
 if [ "$REV" = WORKTREE ]; then
   mkdir -p $T/ray-tracer-challenge-rs_amd
-  cp -r $R/include $T/ && cp -r $R/ray-tracer-challenge-rs_amd/csrc $R/ray-tracer-challenge-rs_amd/Makefile $T/ray-tracer-challenge-rs_amd/
+  cp -r $R/include $T/ && cp -r $R/ray-tracer-challenge-rs_amd/csrc $R/ray-tracer-challenge-rs_amd/tools $R/ray-tracer-challenge-rs_amd/Makefile $T/ray-tracer-challenge-rs_amd/
 else
   (cd $R && git archive "$REV" ray-tracer-challenge-rs_amd include) | tar -x -C $T
 fi

@@ -23,6 +23,7 @@ def main():
         scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{name}.json"))
         cam = rtc_amd.camera_resize(scene.camera, w, h)
         with rtc_amd.Context(0) as ctx:
+            ctx.set_jit(rtc_amd.RT_JIT_SYNC)
             ctx.upload(scene)
             prec = os.environ.get("JIT_PRECISION", "f32")
             out = torch.empty((h, w, 3), dtype=torch.float32 if prec == "f32" else torch.float64, device="cuda")

@@ -18,6 +18,7 @@ scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{name}.j
 cam = rtc_amd.camera_resize(scene.camera, w, h)
 s = torch.cuda.current_stream()
 with rtc_amd.Context(0) as ctx:
+    ctx.set_jit(rtc_amd.RT_JIT_SYNC)  # the per-scene kernels from the first frame (as a warm renderer runs)
     ctx.upload(scene)
     for shards in COUNTS:
         rows = rtc_amd.shard_rows(h, shards)
