@@ -6,22 +6,24 @@ A step is one frame, scene tables and output buffer resident in HBM.  Rays
 are counted on the device in the reference's semantics (SURVEY.md §8d:
 primary + shadow + reflect + refract).
 
-* One GPU (the default): one launch of the persistent tracer over a
-  1920x1080 canvas of scenes/three_sphere_scene.yaml = BASELINE configs[1]
-  (the YAML's camera with width/height overridden, exactly like editing the
-  YAML), f32 framebuffer.
-* N GPUs (python -m torch.distributed.run --nproc-per-node N bench.py
-  --gpus N ...; one process per GPU): by default the north star's image-tile
-  split of BASELINE configs[3] — scenes/cover.yaml at 3840x2160, every frame
+* A step renders configs[1] on every GPU: one launch of the persistent
+  tracer over a 1920x1080 canvas of scenes/three_sphere_scene.yaml (the
+  YAML's camera with width/height overridden, exactly like editing the
+  YAML), f32 framebuffer.  With N GPUs (python -m torch.distributed.run
+  --nproc-per-node N bench.py --gpus N ...; one process per GPU) each GPU
+  renders its own frame per step (independent frames: no data-path
+  collective, "scaling": "weak"), so the line's workload per GPU is the same
+  at every N and `value` is the whole job's rays / time.
+* With N > 1 the default run then also measures the north star's image-tile
+  split, BASELINE configs[3]: scenes/cover.yaml at 3840x2160, every frame
   split across the N GPUs in cyclic row blocks by librtc's own multi-GPU
   context (csrc/rtc_group.cpp: the scene RCCL-broadcast by rt_scene_upload,
   the strips RCCL-gathered onto rank 0 and de-interleaved there), gathering
-  the 8-bit canvas (canvas.rs:117-123; 4x fewer bytes than f32).  "scaling":
-  "strong" (one frame per step, whatever N).  The line also carries the same
-  workload on rank 0's GPU alone (`single_gpu_ms_per_step`) and the frame's
-  per-shard render / gather / end-to-end milliseconds.
-  `--mode frames` instead renders an independent frame per rank per step
-  (no data-path collective, "scaling": "weak").
+  the 8-bit canvas (canvas.rs:117-123; 4x fewer bytes than f32), and attaches
+  it as "tile_split": its Mray/s and ms/frame, per-shard render / gather /
+  end-to-end milliseconds, and the same frame on rank 0's GPU alone
+  (`single_gpu_ms_per_step`, `speedup_vs_1gpu`).  `--mode tiled` makes the
+  split the line itself ("scaling": "strong"); `--mode frames` skips it.
 
 Prints ONE JSON line on rank 0 with the roofline of the tracer kernel (FP32
 VALU roof, algorithmic FLOPs of SURVEY.md §8d) and, on one GPU, the CPU
@@ -55,7 +57,8 @@ def parse():
                     help="keep warming up (untimed) until at least this much wall time of frames has run, "
                          "whatever --warmup: a few 25 us frames leave the GPU below its steady clocks")
     ap.add_argument("--mode", choices=["auto", "frames", "tiled"], default="auto",
-                    help="auto: one GPU renders frames; N > 1 GPUs split each frame (tiled)")
+                    help="auto: a frame per GPU per step, plus (N > 1) the configs[3] tile split as 'tile_split'; "
+                         "frames: without it; tiled: the tile split is the line")
     ap.add_argument("--scene", default=None,
                     help="default three_sphere_scene (configs[1]) on one GPU / in frames mode, cover (configs[3]) "
                          "when tiled")
@@ -169,28 +172,29 @@ def timed_launches(fn, stream, n):
     return run
 
 
+def resolve(args, tiled):
+    """Fill the workload defaults: configs[1] (three_sphere at 1920x1080, f32
+    frames) unless tiled, configs[3] (cover at 3840x2160, u8 canvas) when tiled."""
+    a = argparse.Namespace(**vars(args))
+    if a.scene is None:
+        a.scene = "cover" if tiled else "three_sphere_scene"
+    default_4k = tiled and a.scene == "cover"
+    a.width = a.width or (3840 if default_4k else 1920)
+    a.height = a.height or (2160 if default_4k else 1080)
+    a.out = a.out or ("u8" if tiled else "real")
+    if a.depth is None:
+        a.depth = 5 if a.scene == "three_sphere_scene" else 6
+    return a
+
+
 def main():
     args = parse()
-    import numpy as np
     import torch
     import torch.distributed as dist
-
-    import rtc_amd
-    from rtc_amd import dist as rdist
-    from rtc_amd import scene_io
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    tiled = args.mode == "tiled" or (args.mode == "auto" and world > 1)
-    if args.scene is None:
-        args.scene = "cover" if tiled else "three_sphere_scene"
-    default_4k = tiled and args.scene == "cover"
-    args.width = args.width or (3840 if default_4k else 1920)
-    args.height = args.height or (2160 if default_4k else 1080)
-    args.out = args.out or ("u8" if tiled else "real")
-    if args.depth is None:
-        args.depth = 5 if args.scene == "three_sphere_scene" else 6
     # BENCH_SHARE_GPU=1 rehearses several ranks on a one-GPU box (frames mode;
     # RCCL refuses two ranks on one device, so the tiled group needs one GPU each)
     if os.environ.get("BENCH_SHARE_GPU"):
@@ -200,7 +204,45 @@ def main():
     if world > 1:
         dist.init_process_group("gloo")
     torch.cuda.set_device(local)
+    # The line's workload is the same at every N (the driver divides the
+    # N-GPU value by N x the 1-GPU value): configs[1], one frame per GPU per
+    # step, "weak" (--mode auto|frames).  With N > 1 the auto mode then also
+    # measures the north star's image-tile split of configs[3] (cover at 4K
+    # split across the N GPUs by librtc's RCCL group) and attaches it as
+    # "tile_split"; --mode tiled makes that split the line itself.
+    tiled = args.mode == "tiled"
+    line = measure(resolve(args, tiled), tiled, world, rank, local)
+    if world > 1 and args.mode == "auto":
+        split = measure(resolve(args_for_split(args), True), True, world, rank, local)
+        if rank == 0:
+            line["tile_split"] = {k: split[k] for k in (
+                "value", "unit", "ms_per_step", "steps", "scaling", "config", "render_ms_per_shard", "gather_ms",
+                "frame_ms", "single_gpu_ms_per_step", "speedup_vs_1gpu", "single_gpu_value", "roofline",
+                "first_frame_ms") if k in split}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
+
+def args_for_split(args):
+    """configs[3]'s defaults for the tile-split part of an N > 1 run (the
+    line's own --scene/--width/--height/--out/--depth describe its frames)."""
+    a = argparse.Namespace(**vars(args))
+    a.scene = a.width = a.height = a.out = a.depth = None
+    return a
+
+
+def measure(args, tiled, world, rank, local):
+    """One workload on this rank's GPU (frames) or split across the group
+    (tiled); returns rank 0's JSON line (None elsewhere)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import rtc_amd
+    from rtc_amd import dist as rdist
+    from rtc_amd import scene_io
     # Only rank 0 holds the world, as the reference's single caller does
     t_first = time.perf_counter()
     scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{args.scene}.json")) if rank == 0 else None
@@ -320,6 +362,7 @@ def main():
             dist.barrier()
     else:
         kernel_ms = launch_ms
+    line = None
     if rank == 0:
         flops_per_launch = flops / args.steps
         peak = PEAK_FP32_TFLOPS if args.precision == "f32" else PEAK_FP64_TFLOPS
@@ -391,10 +434,10 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(scene, cam, args.depth, args.cpu_seconds)
             line["cpu_baseline"]["configs0_serial"] = cpu_serial_configs0(min(3.0, args.cpu_seconds / 4))
-        print(json.dumps(line), flush=True)
     ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
+    return line if rank == 0 else None
+
+
 
 
 if __name__ == "__main__":

@@ -69,3 +69,23 @@ def test_bench_pool_scene_reports_cold_launch():
     d = _run("--scene", "reflect_refract", "--steps", "10", "--warmup", "2", "--width", "320", "--height", "240",
              "--no-cpu-baseline")
     assert d["cold_kernel_ms"] > 0 and d["host_frame_ms"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_frames_weak_scaling():
+    """N > 1: one process per GPU (here two ranks rehearsed on the one GPU,
+    BENCH_SHARE_GPU=1): each rank renders its own configs[1] frames, the line
+    is the whole job's rays over the slowest rank's time, "scaling": "weak"."""
+    env = dict(os.environ, BENCH_SHARE_GPU="1", MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--mode", "frames", "--steps", "10", "--warmup", "2", "--width", "320",
+                        "--height", "240"], capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [line for line in r.stdout.splitlines() if line.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["config"]["parallelism"] == "framesx2"
+    assert d["config"]["rays_per_frame"] == 2 * 320 * 240 and "tile_split" not in d
+    # the job's rays: both ranks' frames
+    assert abs(d["value"] * d["ms_per_step"] * 1e-3 - 2 * 2 * 320 * 240 / 1e6) < 1e-6 * d["value"]
