@@ -99,8 +99,13 @@ struct rt_context {
     uint32_t* d_cold_order = nullptr;  // centre-out order + item count, for cold_w x cold_h
     uint32_t cold_w = 0, cold_h = 0;
     // Tiles costing more than split_factor x the mean workgroup load are
-    // handed out in parts (order_tiles); RTC_SPLIT=0 never splits.
-    double split_factor = 1.5;
+    // handed out in parts (order_tiles); RTC_SPLIT=0 never splits.  Round-3
+    // sweep (per-scene kernels, slowest of 8 shards at 4K / 1-GPU frame):
+    // 1.5: cover 0.239 / 1.132 ms, table 0.244 / 1.389; 1.0: 0.217 / 1.142,
+    // 0.226 / 1.369; 0.75: 0.206 / 1.128, 0.233 / 1.384; 0.5: 0.205 / 1.128,
+    // 0.245 / 1.414; reflect_refract 1080p, slowest of 4: 0.146 / 0.129 /
+    // 0.126 / 0.131 with whole frames unchanged (0.385-0.403).
+    double split_factor = 1.0;
     int order_builds = 0;        // order_tiles runs for the current signature so far
     int order_max_builds = 8;    // RTC_ORDER_BUILDS: runs per signature before the order is frozen
     uint64_t scene_gen = 0;      // bumped by every rt_scene_upload
