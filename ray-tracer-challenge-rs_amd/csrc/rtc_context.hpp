@@ -18,24 +18,36 @@
 namespace rtc {
 
 // World tables cast to R and laid out per kind (rtc_internal.hpp).
+// The shape, material and pattern tables and world_slot sit in ONE
+// allocation in the kernels' LDS layout ([shapes][materials][patterns]
+// [world_slot], world_lds_bytes), so a workgroup stages the world into LDS
+// with one contiguous copy (scene_view).
 template <typename R>
 struct DeviceWorld {
+    void* image = nullptr;  // the allocation holding the four tables
     ShapeRec<R>* shapes = nullptr;
     MaterialRec<R>* materials = nullptr;
     PatternRec<R>* patterns = nullptr;
     LightRec<R>* lights = nullptr;
     int32_t* world_slot = nullptr;
     DevScene<R> scene{};
+    // Point the tables into `image` for ns shapes, nm materials, np patterns.
+    void carve(size_t ns, size_t nm, size_t np) {
+        unsigned char* b = static_cast<unsigned char*>(image);
+        shapes = reinterpret_cast<ShapeRec<R>*>(b);
+        materials = reinterpret_cast<MaterialRec<R>*>(b + ns * sizeof(ShapeRec<R>));
+        patterns = reinterpret_cast<PatternRec<R>*>(b + ns * sizeof(ShapeRec<R>) + nm * sizeof(MaterialRec<R>));
+        world_slot = reinterpret_cast<int32_t*>(b + ns * sizeof(ShapeRec<R>) + nm * sizeof(MaterialRec<R>) +
+                                                np * sizeof(PatternRec<R>));
+    }
     void release() {
-        (void)hipFree(world_slot);
-        world_slot = nullptr;
-        (void)hipFree(shapes);
-        (void)hipFree(materials);
-        (void)hipFree(patterns);
+        (void)hipFree(image);
         (void)hipFree(lights);
+        image = nullptr;
         shapes = nullptr;
         materials = nullptr;
         patterns = nullptr;
+        world_slot = nullptr;
         lights = nullptr;
     }
 };

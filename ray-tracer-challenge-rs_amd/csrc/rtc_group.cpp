@@ -7,7 +7,8 @@
 // here, not in the caller:
 //
 //   rt_scene_upload   rank 0 flattens the World (rtc_host.cpp build_scene)
-//                     and ncclBroadcasts a header plus the ten device tables
+//                     and ncclBroadcasts a header plus the four device
+//                     buffers (per precision: the table image, the lights)
 //                     (f32 and f64 records) to every other GPU.
 //   rt_render[_device] every member renders its shard — cyclic RT_TILE_H-row
 //                     blocks (rank r takes tile rows r, r+G, ...), which
@@ -63,15 +64,9 @@ struct SceneHeader {
 template <typename R>
 int alloc_world(DeviceWorld<R>& w, const SceneHeader& h) {
     w.release();
-    auto get = [](auto** p, size_t n) -> int {
-        *p = nullptr;
-        if (n) RT_HIP(hipMalloc(reinterpret_cast<void**>(p), n * sizeof(**p)));
-        return RT_OK;
-    };
-    int rc;
-    if ((rc = get(&w.shapes, h.ns)) || (rc = get(&w.materials, h.nm)) || (rc = get(&w.patterns, h.np)) ||
-        (rc = get(&w.lights, h.nl)) || (rc = get(&w.world_slot, (h.ns + 3) / 4 * 4)))
-        return rc;
+    RT_HIP(hipMalloc(&w.image, std::max<size_t>(world_lds_bytes<R>(h.ns, h.nm, h.np), 16)));
+    w.carve(h.ns, h.nm, h.np);
+    if (h.nl) RT_HIP(hipMalloc(reinterpret_cast<void**>(&w.lights), h.nl * sizeof(LightRec<R>)));
     return RT_OK;
 }
 
@@ -93,11 +88,8 @@ void describe_world(DeviceWorld<R>& w, const SceneHeader& h) {
 // on every rank.
 template <typename R>
 void world_buffers(DeviceWorld<R>& w, const SceneHeader& h, std::vector<std::pair<void*, size_t>>& out) {
-    out.push_back({w.shapes, h.ns * sizeof(ShapeRec<R>)});
-    out.push_back({w.materials, h.nm * sizeof(MaterialRec<R>)});
-    out.push_back({w.patterns, h.np * sizeof(PatternRec<R>)});
+    out.push_back({w.image, world_lds_bytes<R>(h.ns, h.nm, h.np)});  // shapes, materials, patterns, world_slot
     out.push_back({w.lights, h.nl * sizeof(LightRec<R>)});
-    out.push_back({w.world_slot, (h.ns + 3) / 4 * 4 * sizeof(int32_t)});
 }
 
 int ensure(void** p, size_t* have, size_t need) {

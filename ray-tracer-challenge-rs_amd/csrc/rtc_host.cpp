@@ -233,9 +233,22 @@ int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes,
             lt[i].intensity[q] = (R)lights[i].intensity[q];
         }
     int rc;
-    if ((rc = upload(&w.shapes, sh)) || (rc = upload(&w.materials, mt)) || (rc = upload(&w.patterns, pt)) ||
-        (rc = upload(&w.lights, lt)) || (rc = upload(&w.world_slot, ws)))
-        return rc;
+    // shapes, materials, patterns and world_slot in one allocation, in the LDS layout
+    const size_t image_bytes = world_lds_bytes<R>(sh.size(), nm, np);
+    std::vector<unsigned char> img(image_bytes);
+    size_t at = 0;
+    auto put = [&](const void* src, size_t n) {
+        if (n) std::memcpy(img.data() + at, src, n);
+        at += n;
+    };
+    put(sh.data(), sh.size() * sizeof(ShapeRec<R>));
+    put(mt.data(), mt.size() * sizeof(MaterialRec<R>));
+    put(pt.data(), pt.size() * sizeof(PatternRec<R>));
+    put(ws.data(), ws.size() * sizeof(int32_t));
+    RT_HIP(hipMalloc(&w.image, std::max<size_t>(image_bytes, 16)));  // (an empty world still gets a buffer)
+    if (image_bytes) RT_HIP(hipMemcpy(w.image, img.data(), image_bytes, hipMemcpyHostToDevice));
+    w.carve(sh.size(), nm, np);
+    if ((rc = upload(&w.lights, lt))) return rc;
     ctx->world_slot.assign(ws.begin(), ws.begin() + ns);
     w.scene.shapes = w.shapes;
     w.scene.materials = w.materials;

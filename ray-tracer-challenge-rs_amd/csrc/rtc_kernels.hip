@@ -1174,15 +1174,14 @@ __device__ inline DevScene<R> scene_view(const LaunchParams<R>& P, const ShapeRe
         auto* lp = reinterpret_cast<PatternRec<R>*>(lm + sc.n_materials);
         auto* lw = reinterpret_cast<int32_t*>(lp + sc.n_patterns);
         if (stage) {
-            auto copy = [](void* dst, const void* src, uint32_t bytes) {
-                const uint4* s4 = static_cast<const uint4*>(src);
-                uint4* d4 = static_cast<uint4*>(dst);
-                for (uint32_t i = threadIdx.x; i < bytes / 16; i += kBlock) d4[i] = s4[i];
-            };
-            copy(ls, shapes, ns * (uint32_t)sizeof(ShapeRec<R>));
-            copy(lm, materials, sc.n_materials * (uint32_t)sizeof(MaterialRec<R>));
-            copy(lp, patterns, sc.n_patterns * (uint32_t)sizeof(PatternRec<R>));
-            copy(lw, sc.world_slot, (ns + 3) / 4 * 16);
+            // The four tables are one allocation in this very layout
+            // (rtc_context.hpp DeviceWorld), starting at `shapes`: one
+            // contiguous copy, all loads in flight before the first LDS
+            // write (four table-by-table loops waited on four load
+            // latencies, in every one of the direct kernel's 5120 workgroups).
+            const uint4* s4 = reinterpret_cast<const uint4*>(shapes);
+            uint4* d4 = reinterpret_cast<uint4*>(ls);
+            for (uint32_t i = threadIdx.x; i < P.world_lds / 16; i += kBlock) d4[i] = s4[i];
             __syncthreads();
         }
         sc.lworld_slot = lw;
