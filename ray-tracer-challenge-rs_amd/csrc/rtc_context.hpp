@@ -118,6 +118,7 @@ struct rt_context {
     // 0.245 / 1.414; reflect_refract 1080p, slowest of 4: 0.146 / 0.129 /
     // 0.126 / 0.131 with whole frames unchanged (0.385-0.403).
     double split_factor = 1.0;
+    uint32_t split_max = 2;      // RTC_SPLIT_MAX: log2 of the most parts a tile is split into
     int order_builds = 0;        // order_tiles runs for the current signature so far
     int order_max_builds = 8;    // RTC_ORDER_BUILDS: runs per signature before the order is frozen
     uint64_t scene_gen = 0;      // bumped by every rt_scene_upload

@@ -71,11 +71,12 @@ constexpr int kTileQueues = 8;
 // dequeues on MI355X).
 constexpr int kQueueStride = 32;
 // Work items of a cost-ordered pool launch: a tile, or one part of a tile
-// split 2 or 4 ways (order_tiles).  item = tile | part << 24 | log2(parts) << 28;
-// part p of a tile split 2^l ways seeds the pixels of waves w with
-// w >> (2 - l) == p.
+// split 2, 4 or 8 ways (order_tiles).  item = tile | part << 24 | log2(parts)
+// << 27; part p of a tile split 2^l ways seeds the pixels of threads t with
+// t >> (8 - l) == p (halves, wave pairs, waves, half-waves).
 constexpr uint32_t kItemTileMask = 0xFFFFFFu;
-constexpr uint32_t kItemPartShift = 24, kItemSplitShift = 28;
+constexpr uint32_t kItemPartShift = 24, kItemSplitShift = 27, kItemPartMask = 7u;
+constexpr uint32_t kMaxSplitLog2 = 3;  // up to 8 items per tile
 // Tile scheduling modes (RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic)
 constexpr uint32_t kSchedGrid = 0;     // one workgroup per tile; the dispatcher balances
 constexpr uint32_t kSchedDynamic = 1;  // resident grid, per-XCD atomic tile queues

@@ -1447,7 +1447,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         uint64_t out_idx;
         load_primary(P, t, tid, valid, o, d, out_idx);
         // this item's part of the tile (all of it unless split)
-        valid &= ((tid >> 6) >> (2 - split)) == ((item >> kItemPartShift) & 3u);
+        valid &= (tid >> (8 - split)) == ((item >> kItemPartShift) & kItemPartMask);
         k.c[0] += wave_count(valid);
         {
             const int slot = wave_reserve(valid, &s_top[0]);
@@ -1525,7 +1525,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
 // affected.
 //
 // A tile costing more than split_factor x the mean workgroup load (sum of
-// costs / grid) is handed out as 2 or 4 parts (items, rtc_internal.hpp): when
+// costs / grid) is handed out as 2, 4 (or 8, RTC_SPLIT_MAX=3) parts (items, rtc_internal.hpp): when
 // a launch has few tiles per workgroup (a shard of a multi-GPU frame) its
 // heaviest tiles outlast everything else, and the parts of one run on
 // different CUs.  The parts' seeds cover a quarter or half of the tile, and
@@ -1539,14 +1539,18 @@ __device__ inline uint32_t cost_bucket(uint32_t c) {  // 0 = heaviest
     return (uint32_t)(kOrderBuckets - 1) - (b < (uint32_t)kOrderBuckets ? b : (uint32_t)(kOrderBuckets - 1));
 }
 
-// log2 of the parts a tile of cost c is split into (0, 1 or 2)
-__device__ inline uint32_t split_log2(uint32_t c, float limit) {
-    return (float)c > 2.0f * limit ? 2u : ((float)c > limit ? 1u : 0u);
+// log2 of the parts a tile of cost c is split into: the least l with
+// c / 2^l <= limit, at most max_log2
+__device__ inline uint32_t split_log2(uint32_t c, float limit, uint32_t max_log2) {
+    uint32_t l = 0;
+    while (l < max_log2 && (float)c > limit * (float)(1u << l)) ++l;
+    return l;
 }
 
 __global__ __launch_bounds__(kOrderThreads) void order_tiles(uint32_t* __restrict__ cost,
                                                              uint32_t* __restrict__ order, uint32_t n,
-                                                             uint32_t* __restrict__ n_items, float split_per_cost) {
+                                                             uint32_t* __restrict__ n_items, float split_per_cost,
+                                                             uint32_t max_log2) {
     __shared__ uint32_t hist[kOrderBuckets];
     __shared__ uint32_t scan[kOrderBuckets];
     __shared__ unsigned long long total;
@@ -1573,7 +1577,7 @@ __global__ __launch_bounds__(kOrderThreads) void order_tiles(uint32_t* __restric
     }
     unsigned long long mine_items = 0;
     for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) {
-        const uint32_t c = cost[i], l = split_log2(c, limit);
+        const uint32_t c = cost[i], l = split_log2(c, limit, max_log2);
         atomicAdd(&hist[cost_bucket(c >> l)], 1u << l);
         mine_items += 1u << l;
     }
@@ -1598,7 +1602,7 @@ __global__ __launch_bounds__(kOrderThreads) void order_tiles(uint32_t* __restric
     if (t < (uint32_t)kOrderBuckets) hist[t] = scan[t] - own;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) {
-        const uint32_t c = cost[i], l = split_log2(c, limit);
+        const uint32_t c = cost[i], l = split_log2(c, limit, max_log2);
         const uint32_t pos = atomicAdd(&hist[cost_bucket(c >> l)], 1u << l);
         for (uint32_t p = 0; p < (1u << l); ++p) order[pos + p] = i | p << kItemPartShift | l << kItemSplitShift;
         if (l) cost[i] = 0;
@@ -1736,9 +1740,10 @@ template hipError_t occupancy<double>(bool, bool, size_t, int*);
 
 #if RTC_PRECISION != 2
 hipError_t launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, uint32_t* n_items, float split_per_cost,
-                              hipStream_t stream) {
+                              uint32_t max_split_log2, hipStream_t stream) {
     (void)hipGetLastError();  // see launch_trace
-    hipLaunchKernelGGL(order_tiles, dim3(1), dim3(kOrderThreads), 0, stream, cost, order, n, n_items, split_per_cost);
+    hipLaunchKernelGGL(order_tiles, dim3(1), dim3(kOrderThreads), 0, stream, cost, order, n, n_items, split_per_cost,
+                       max_split_log2);
     return hipGetLastError();
 }
 #endif
