@@ -119,6 +119,16 @@ struct rt_context {
     // 0.126 / 0.131 with whole frames unchanged (0.385-0.403).
     double split_factor = 1.0;
     uint32_t split_max = 2;      // RTC_SPLIT_MAX: log2 of the most parts a tile is split into
+    // Items (tiles or parts) costing more than urgent_factor x the mean
+    // workgroup load run at raised wave priority, graded 1/2/3 above 1x/2x/4x
+    // that cost (RTC_URGENT, 0 = none; RTC_URGENT_GRADED=0: priority 3 for
+    // all of them).  Same-box sweep, kernel ms, none / flat 0.25 / flat 0.125 /
+    // graded 0.125: reflect_refract 0.367 / 0.310 / 0.306 / 0.310, cylinders
+    // 0.124 / 0.117 / 0.117 / 0.117, cover 4K 1.014 / 1.023 / 1.011 / 1.011,
+    // table 4K, refraction, metal within 1 %; slowest of 8 shards at 4K: cover
+    // 0.215 / 0.201 / 0.215 / 0.201, table 0.229 / 0.266 / 0.230 / 0.231.
+    double urgent_factor = 0.125;
+    bool urgent_graded = true;
     int order_builds = 0;        // order_tiles runs for the current signature so far
     int order_max_builds = 8;    // RTC_ORDER_BUILDS: runs per signature before the order is frozen
     uint64_t scene_gen = 0;      // bumped by every rt_scene_upload

@@ -41,7 +41,7 @@ hipError_t launch_trace(const LaunchParams<R>& P, bool pool, bool dup, uint32_t 
 constexpr uint32_t kKindsSp = (1u << RT_SHAPE_SPHERE) | (1u << RT_SHAPE_PLANE);
 
 hipError_t launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, uint32_t* n_items, float split_per_cost,
-                              uint32_t max_split_log2, hipStream_t stream);
+                              uint32_t max_split_log2, float urgent_per_cost, uint32_t graded, hipStream_t stream);
 template <typename R>
 hipError_t launch_debug_shape(const ShapeRec<R>* shapes, int slot, int kind, uint32_t mode, uint32_t world_space,
                               const double* in, uint32_t n, double* out, hipStream_t stream);
@@ -461,8 +461,9 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
     uint32_t* n_items = ctx->d_tile_order + ((size_t)ctx->order_capacity << kMaxSplitLog2);
     if ((same || moved) && ctx->order_builds < ctx->order_max_builds) {
         const float split = ctx->split_factor > 0 ? (float)(ctx->split_factor / grid) : 0.0f;
+        const float urgent = ctx->urgent_factor > 0 ? (float)(ctx->urgent_factor / grid) : 0.0f;
         RT_HIP(launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, P.n_tiles, n_items, split, ctx->split_max,
-                                  stream));
+                                  urgent, ctx->urgent_graded, stream));
         ++ctx->order_builds;
         ctx->order_built = true;
     }
@@ -795,6 +796,8 @@ int create_device_context(int device_ordinal, rt_context** out) {
     if (const char* e = std::getenv("RTC_SPLIT")) ctx->split_factor = std::atof(e);
     if (const char* e = std::getenv("RTC_SPLIT_MAX"))
         ctx->split_max = (uint32_t)std::min<int>((int)kMaxSplitLog2, std::max(0, std::atoi(e)));
+    if (const char* e = std::getenv("RTC_URGENT")) ctx->urgent_factor = std::atof(e);
+    if (const char* e = std::getenv("RTC_URGENT_GRADED")) ctx->urgent_graded = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_ORDER_BUILDS")) ctx->order_max_builds = std::atoi(e);
     if (const char* e = std::getenv("RTC_DIRECT_GRID")) ctx->direct_grid = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("RTC_JIT"))

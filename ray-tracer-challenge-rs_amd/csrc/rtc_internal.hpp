@@ -72,10 +72,13 @@ constexpr int kTileQueues = 8;
 constexpr int kQueueStride = 32;
 // Work items of a cost-ordered pool launch: a tile, or one part of a tile
 // split 2, 4 or 8 ways (order_tiles).  item = tile | part << 24 | log2(parts)
-// << 27; part p of a tile split 2^l ways seeds the pixels of threads t with
-// t >> (8 - l) == p (halves, wave pairs, waves, half-waves).
+// << 27 | priority << 29; part p of a tile split 2^l ways seeds the pixels of
+// threads t with t >> (8 - l) == p (halves, wave pairs, waves, half-waves).
+// An item of priority p > 0 (the costliest, order_tiles) runs its waves at
+// s_setprio(p).
 constexpr uint32_t kItemTileMask = 0xFFFFFFu;
-constexpr uint32_t kItemPartShift = 24, kItemSplitShift = 27, kItemPartMask = 7u;
+constexpr uint32_t kItemPartShift = 24, kItemSplitShift = 27, kItemPartMask = 7u, kItemSplitMask = 3u;
+constexpr uint32_t kItemPrioShift = 29;
 constexpr uint32_t kMaxSplitLog2 = 3;  // up to 8 items per tile
 // Tile scheduling modes (RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic)
 constexpr uint32_t kSchedGrid = 0;     // one workgroup per tile; the dispatcher balances

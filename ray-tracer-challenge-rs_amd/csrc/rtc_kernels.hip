@@ -1441,7 +1441,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         __syncthreads();
         const uint32_t item = __builtin_amdgcn_readfirstlane(s_tile[it & 1]);
         if (item == 0xFFFFFFFFu) break;
-        const uint32_t t = item & kItemTileMask, split = item >> kItemSplitShift;
+        const uint32_t t = item & kItemTileMask, split = (item >> kItemSplitShift) & kItemSplitMask;
+        // the costliest items set the launch's tail: their waves win issue
+        // arbitration against the other workgroups' on the same SIMDs
+        const uint32_t prio = (item >> kItemPrioShift) & 3u;
+        if (prio == 1) __builtin_amdgcn_s_setprio(1);
+        else if (prio == 2) __builtin_amdgcn_s_setprio(2);
+        else if (prio == 3) __builtin_amdgcn_s_setprio(3);
         bool valid;
         V3<R> o, d;
         uint64_t out_idx;
@@ -1495,6 +1501,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         const V3<R> c = {(R)((double)pl.acc[tid] * kAccInvScale), (R)((double)pl.acc[kBlock + tid] * kAccInvScale),
                          (R)((double)pl.acc[2 * kBlock + tid] * kAccInvScale)};
         if (valid) store_pixel(P, out_idx, c);
+        if (prio) __builtin_amdgcn_s_setprio(0);
         __syncthreads();  // accumulators are re-zeroed for the next tile
         // this tile's cost (10 ns ticks) orders the next launch of the same
         // frame heaviest-first (order_tiles)
@@ -1550,7 +1557,8 @@ __device__ inline uint32_t split_log2(uint32_t c, float limit, uint32_t max_log2
 __global__ __launch_bounds__(kOrderThreads) void order_tiles(uint32_t* __restrict__ cost,
                                                              uint32_t* __restrict__ order, uint32_t n,
                                                              uint32_t* __restrict__ n_items, float split_per_cost,
-                                                             uint32_t max_log2) {
+                                                             uint32_t max_log2, float urgent_per_cost,
+                                                             uint32_t graded) {
     __shared__ uint32_t hist[kOrderBuckets];
     __shared__ uint32_t scan[kOrderBuckets];
     __shared__ unsigned long long total;
@@ -1566,14 +1574,15 @@ __global__ __launch_bounds__(kOrderThreads) void order_tiles(uint32_t* __restric
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         return v;
     };
-    float limit = __FLT_MAX__;  // split nothing
-    if (split_per_cost > 0.0f) {
+    float limit = __FLT_MAX__, urgent = __FLT_MAX__;  // split nothing, nothing urgent
+    if (split_per_cost > 0.0f || urgent_per_cost > 0.0f) {
         unsigned long long mine = 0;
         for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) mine += cost[i];
         mine = wave_sum(mine);
         if ((threadIdx.x & 63) == 0) atomicAdd(&total, mine);
         __syncthreads();
-        limit = (float)total * split_per_cost;
+        if (split_per_cost > 0.0f) limit = (float)total * split_per_cost;
+        if (urgent_per_cost > 0.0f) urgent = (float)total * urgent_per_cost;
     }
     unsigned long long mine_items = 0;
     for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) {
@@ -1604,7 +1613,12 @@ __global__ __launch_bounds__(kOrderThreads) void order_tiles(uint32_t* __restric
     for (uint32_t i = threadIdx.x; i < n; i += kOrderThreads) {
         const uint32_t c = cost[i], l = split_log2(c, limit, max_log2);
         const uint32_t pos = atomicAdd(&hist[cost_bucket(c >> l)], 1u << l);
-        for (uint32_t p = 0; p < (1u << l); ++p) order[pos + p] = i | p << kItemPartShift | l << kItemSplitShift;
+        // priority: 3 above the urgent cost, or graded 1/2/3 above 1x/2x/4x it
+        const float pc = (float)(c >> l);
+        const uint32_t pr = !(pc > urgent) ? 0u : !graded ? 3u : pc > 4.0f * urgent ? 3u : pc > 2.0f * urgent ? 2u : 1u;
+        const uint32_t flag = pr << kItemPrioShift;
+        for (uint32_t p = 0; p < (1u << l); ++p)
+            order[pos + p] = i | p << kItemPartShift | l << kItemSplitShift | flag;
         if (l) cost[i] = 0;
     }
     if (threadIdx.x == 0) *n_items = items;
@@ -1740,10 +1754,10 @@ template hipError_t occupancy<double>(bool, bool, size_t, int*);
 
 #if RTC_PRECISION != 2
 hipError_t launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, uint32_t* n_items, float split_per_cost,
-                              uint32_t max_split_log2, hipStream_t stream) {
+                              uint32_t max_split_log2, float urgent_per_cost, uint32_t graded, hipStream_t stream) {
     (void)hipGetLastError();  // see launch_trace
     hipLaunchKernelGGL(order_tiles, dim3(1), dim3(kOrderThreads), 0, stream, cost, order, n, n_items, split_per_cost,
-                       max_split_log2);
+                       max_split_log2, urgent_per_cost, graded);
     return hipGetLastError();
 }
 #endif
