@@ -413,8 +413,8 @@ def measure(args, tiled, world, rank, local):
             pass
         if not tiled and world == 1:
             if ctx.scene.has_secondary() and args.depth > 0:
-                # cold launch: the first frame after an upload runs tiles in
-                # raster order (no recorded costs to order them heaviest-first)
+                # cold launch: the first frame after an upload has no recorded
+                # tile costs; its order comes from the cost probe
                 cold = []
                 for _ in range(3):
                     ctx.upload(scene)

@@ -129,6 +129,12 @@ struct rt_context {
     // 0.215 / 0.201 / 0.215 / 0.201, table 0.229 / 0.266 / 0.230 / 0.231.
     double urgent_factor = 0.125;
     bool urgent_graded = true;
+    // The first launch of a frame geometry orders its tiles by estimated
+    // costs (probe_tiles: per sampled primary hit 1 + wr x reflective + wt x
+    // transparent), split by them if probe_split (RTC_COLD_PROBE=0 | wr,wt,split).
+    bool cold_probe = true;
+    float probe_wr = 8.0f, probe_wt = 24.0f;
+    bool probe_split = false;
     int order_builds = 0;        // order_tiles runs for the current signature so far
     int order_max_builds = 8;    // RTC_ORDER_BUILDS: runs per signature before the order is frozen
     uint64_t scene_gen = 0;      // bumped by every rt_scene_upload

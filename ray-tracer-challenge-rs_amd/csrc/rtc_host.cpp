@@ -40,6 +40,8 @@ hipError_t launch_trace(const LaunchParams<R>& P, bool pool, bool dup, uint32_t 
 }  // namespace sp
 constexpr uint32_t kKindsSp = (1u << RT_SHAPE_SPHERE) | (1u << RT_SHAPE_PLANE);
 
+template <typename R>
+hipError_t launch_probe(const LaunchParams<R>& P, float wr, float wt, hipStream_t stream);
 hipError_t launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, uint32_t* n_items, float split_per_cost,
                               uint32_t max_split_log2, float urgent_per_cost, uint32_t graded, hipStream_t stream);
 template <typename R>
@@ -292,11 +294,13 @@ uint32_t tile_rows_for(uint32_t height, uint32_t shards, uint32_t shard) {
 }
 
 // Rays held by the LDS pool for a given depth and pop batch (LIFO bound).
-uint32_t pool_capacity(uint32_t depth, uint32_t batch) { return (uint32_t)kBlock + depth * batch; }
+// (RTC_OVERLAP: the next item's seeds land on a pool of fewer than a batch of
+// the previous item's rays)
+uint32_t pool_capacity(uint32_t depth, uint32_t batch) { return (uint32_t)kBlock * kAccSlots + depth * batch; }
 
 template <typename R>
 size_t pool_lds_bytes(uint32_t cap) {
-    return 3 * kBlock * sizeof(long long) + (size_t)cap * (7 * sizeof(R) + sizeof(uint32_t));
+    return kAccSlots * 3 * kBlock * sizeof(long long) + (size_t)cap * (7 * sizeof(R) + sizeof(uint32_t));
 }
 
 constexpr size_t kLdsPerCu = 160 * 1024;
@@ -465,6 +469,16 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
         RT_HIP(launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, P.n_tiles, n_items, split, ctx->split_max,
                                   urgent, ctx->urgent_graded, stream));
         ++ctx->order_builds;
+        ctx->order_built = true;
+    }
+    if (!ctx->order_built && ctx->cold_probe) {
+        // No costs yet: estimate them (probe_tiles) and order by the estimate.
+        P.tile_cost = ctx->d_tile_cost;
+        RT_HIP(launch_probe<R>(P, ctx->probe_wr, ctx->probe_wt, stream));
+        const float split = ctx->split_factor > 0 && ctx->probe_split ? (float)(ctx->split_factor / grid) : 0.0f;
+        const float urgent = ctx->urgent_factor > 0 ? (float)(ctx->urgent_factor / grid) : 0.0f;
+        RT_HIP(launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, P.n_tiles, n_items, split, ctx->split_max,
+                                  urgent, ctx->urgent_graded, stream));
         ctx->order_built = true;
     }
     if (ctx->order_built) {  // built from this frame's costs, or from the previous camera's frame
@@ -797,6 +811,17 @@ int create_device_context(int device_ordinal, rt_context** out) {
     if (const char* e = std::getenv("RTC_SPLIT_MAX"))
         ctx->split_max = (uint32_t)std::min<int>((int)kMaxSplitLog2, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("RTC_URGENT")) ctx->urgent_factor = std::atof(e);
+    if (const char* e = std::getenv("RTC_COLD_PROBE")) {  // 0 = off, or "wr,wt[,split]"
+        ctx->cold_probe = std::strcmp(e, "0") != 0;
+        float wr = 0, wt = 0;
+        int sp = 0;
+        const int n = std::sscanf(e, "%f,%f,%d", &wr, &wt, &sp);
+        if (n >= 2) {
+            ctx->probe_wr = wr;
+            ctx->probe_wt = wt;
+        }
+        if (n >= 3) ctx->probe_split = sp != 0;
+    }
     if (const char* e = std::getenv("RTC_URGENT_GRADED")) ctx->urgent_graded = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_ORDER_BUILDS")) ctx->order_max_builds = std::atoi(e);
     if (const char* e = std::getenv("RTC_DIRECT_GRID")) ctx->direct_grid = (uint32_t)std::atoi(e);

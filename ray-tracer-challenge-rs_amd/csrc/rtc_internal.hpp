@@ -79,6 +79,11 @@ constexpr int kQueueStride = 32;
 constexpr uint32_t kItemTileMask = 0xFFFFFFu;
 constexpr uint32_t kItemPartShift = 24, kItemSplitShift = 27, kItemPartMask = 7u, kItemSplitMask = 3u;
 constexpr uint32_t kItemPrioShift = 29;
+// Pool kernel with two items' rays in flight at once (trace_pool): 2 accumulator slots.
+#ifndef RTC_OVERLAP
+#define RTC_OVERLAP 0
+#endif
+constexpr uint32_t kAccSlots = RTC_OVERLAP ? 2 : 1;
 constexpr uint32_t kMaxSplitLog2 = 3;  // up to 8 items per tile
 // Tile scheduling modes (RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic)
 constexpr uint32_t kSchedGrid = 0;     // one workgroup per tile; the dispatcher balances

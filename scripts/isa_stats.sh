@@ -3,8 +3,9 @@
 # instruction-class counts per kernel (CPU-side; no GPU needed).
 set -e
 OUT=${1:-/tmp/rtc_isa.s}
+shift || true
 cd "$(dirname "$0")/../ray-tracer-challenge-rs_amd"
-/opt/rocm/bin/hipcc -O3 -std=c++20 --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize --cuda-device-only -S \
+/opt/rocm/bin/hipcc -O3 -std=c++20 --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize --cuda-device-only -S "$@" \
     -o "$OUT" csrc/rtc_kernels.hip
 python3 - "$OUT" <<'PY'
 import re, sys
