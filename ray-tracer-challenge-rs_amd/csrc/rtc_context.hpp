@@ -118,7 +118,12 @@ struct rt_context {
     // 0.245 / 1.414; reflect_refract 1080p, slowest of 4: 0.146 / 0.129 /
     // 0.126 / 0.131 with whole frames unchanged (0.385-0.403).
     double split_factor = 1.0;
-    uint32_t split_max = 2;      // RTC_SPLIT_MAX: log2 of the most parts a tile is split into
+    // RTC_SPLIT_MAX: log2 of the most parts a tile is split into.  Same-box
+    // sweep (profiles/r03_split16_sweep.txt, r03_shard_floor.txt), slowest
+    // shard ms at 2 / 3 / 4: cover 4K of 8 0.198 / 0.202 / 0.207, of 32
+    // 0.130 / 0.096 / 0.115; reflect_refract 1080p of 4 0.127 / 0.128 /
+    // 0.121, of 16 0.112 / 0.092 / 0.097; whole frames split nothing.
+    uint32_t split_max = 3;
     // Items (tiles or parts) costing more than urgent_factor x the mean
     // workgroup load run at raised wave priority, graded 1/2/3 above 1x/2x/4x
     // that cost (RTC_URGENT, 0 = none; RTC_URGENT_GRADED=0: priority 3 for

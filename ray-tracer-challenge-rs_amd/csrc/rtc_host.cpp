@@ -436,6 +436,7 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
 template <typename R>
 int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* cam, uint32_t depth, uint32_t grid,
                     hipStream_t stream) {
+    if (P.n_tiles > kItemTileMask + 1) return RT_OK;  // items carry 20 tile bits: raster order
     uint64_t h = 1469598103934665603ull;  // FNV-1a
     auto mix = [&h](const void* p, size_t n) {
         const unsigned char* b = static_cast<const unsigned char*>(p);

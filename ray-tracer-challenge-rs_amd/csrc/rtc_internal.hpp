@@ -71,20 +71,22 @@ constexpr int kTileQueues = 8;
 // dequeues on MI355X).
 constexpr int kQueueStride = 32;
 // Work items of a cost-ordered pool launch: a tile, or one part of a tile
-// split 2, 4 or 8 ways (order_tiles).  item = tile | part << 24 | log2(parts)
-// << 27 | priority << 29; part p of a tile split 2^l ways seeds the pixels of
-// threads t with t >> (8 - l) == p (halves, wave pairs, waves, half-waves).
+// split 2, 4, 8 or 16 ways (order_tiles).  item = tile | part << 20 |
+// log2(parts) << 24 | priority << 27; part p of a tile split 2^l ways seeds
+// the pixels of threads t with t >> (8 - l) == p (halves, wave pairs, waves,
+// half-waves, wave rows).  Cost-ordered launches need n_tiles <= 2^20
+// (plan_tile_order; larger frames keep raster order).
 // An item of priority p > 0 (the costliest, order_tiles) runs its waves at
 // s_setprio(p).
-constexpr uint32_t kItemTileMask = 0xFFFFFFu;
-constexpr uint32_t kItemPartShift = 24, kItemSplitShift = 27, kItemPartMask = 7u, kItemSplitMask = 3u;
-constexpr uint32_t kItemPrioShift = 29;
+constexpr uint32_t kItemTileMask = 0xFFFFFu;
+constexpr uint32_t kItemPartShift = 20, kItemSplitShift = 24, kItemPartMask = 15u, kItemSplitMask = 7u;
+constexpr uint32_t kItemPrioShift = 27;
 // Pool kernel with two items' rays in flight at once (trace_pool): 2 accumulator slots.
 #ifndef RTC_OVERLAP
 #define RTC_OVERLAP 0
 #endif
 constexpr uint32_t kAccSlots = RTC_OVERLAP ? 2 : 1;
-constexpr uint32_t kMaxSplitLog2 = 3;  // up to 8 items per tile
+constexpr uint32_t kMaxSplitLog2 = 4;  // up to 16 items per tile
 // Tile scheduling modes (RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic)
 constexpr uint32_t kSchedGrid = 0;     // one workgroup per tile; the dispatcher balances
 constexpr uint32_t kSchedDynamic = 1;  // resident grid, per-XCD atomic tile queues

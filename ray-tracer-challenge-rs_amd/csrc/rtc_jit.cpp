@@ -201,11 +201,11 @@ jitfile::Request make_request(const std::string& scene, const char* name, const 
     // -3.6 %, three_sphere 4K -2.5 %, 1080p -0.6 %; the pool kernel lost 15 %
     // on cover that way and keeps a fence per shape.
     if (!std::strstr(name, "pool")) rq.opts.push_back("-DRTC_JIT_FENCE_EVERY=3");
-    // RTC_JIT_FLAGS: extra compiler options, space-separated (A/B diagnostics)
+    // RTC_JIT_FLAGS: extra compiler options, space- or comma-separated (A/B diagnostics)
     if (const char* e = std::getenv("RTC_JIT_FLAGS")) {
         const std::string all(e);
         for (size_t p = 0; p < all.size();) {
-            size_t q = all.find(' ', p);
+            size_t q = all.find_first_of(" ,", p);
             if (q == std::string::npos) q = all.size();
             if (q > p) rq.opts.push_back(all.substr(p, q - p));
             p = q + 1;

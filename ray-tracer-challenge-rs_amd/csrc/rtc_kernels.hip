@@ -1581,7 +1581,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
                     if (P.tile_cost) {
                         const uint32_t t = item & kItemTileMask, split = (item >> kItemSplitShift) & kItemSplitMask;
                         const uint32_t c =
-                            (uint32_t)min(__builtin_amdgcn_s_memrealtime() - (s ? start1 : start0), 0x3FFFFFFFull);
+                            (uint32_t)min(__builtin_amdgcn_s_memrealtime() - (s ? start1 : start0), 0x0FFFFFFFull);
                         if (split) atomicMax(&P.tile_cost[t], c << split);
                         else P.tile_cost[t] = c;
                     }
@@ -1706,7 +1706,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         // frame heaviest-first (order_tiles)
         // (a split tile: its slowest part times the parts, order_tiles zeroed it)
         if (tid == 0 && P.tile_cost) {
-            const uint32_t c = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - tile_start, 0x3FFFFFFFull);
+            const uint32_t c = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - tile_start, 0x0FFFFFFFull);
             if (split) atomicMax(&P.tile_cost[t], c << split);
             else P.tile_cost[t] = c;
         }
@@ -1767,7 +1767,7 @@ __global__ __launch_bounds__(kBlock) void probe_tiles(LaunchParams<R> P, RTC_WOR
 // affected.
 //
 // A tile costing more than split_factor x the mean workgroup load (sum of
-// costs / grid) is handed out as 2, 4 (or 8, RTC_SPLIT_MAX=3) parts (items, rtc_internal.hpp): when
+// costs / grid) is handed out as 2, 4 (8 or 16: RTC_SPLIT_MAX=3, 4) parts (items, rtc_internal.hpp): when
 // a launch has few tiles per workgroup (a shard of a multi-GPU frame) its
 // heaviest tiles outlast everything else, and the parts of one run on
 // different CUs.  The parts' seeds cover a quarter or half of the tile, and

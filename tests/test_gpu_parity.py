@@ -236,8 +236,8 @@ def test_cost_ordered_schedule_is_exact(gpu_ctx, rtc, monkeypatch, name):
 @pytest.mark.parametrize("shard", [(0, 1), (1, 4)])
 @pytest.mark.parametrize("name", ["reflect_refract", "cover"])
 def test_split_tiles_are_exact(rtc, monkeypatch, name, shard):
-    """Heavy tiles handed out in 2, 4 or 8 parts (order_tiles; RTC_SPLIT tiny
-    splits nearly every tile 4 (RTC_SPLIT_MAX=3: 8) ways, at 1 every tile above the mean load),
+    """Heavy tiles handed out in 2, 4, 8 or 16 parts (order_tiles; RTC_SPLIT tiny
+    splits nearly every tile 4 (RTC_SPLIT_MAX=3: 8, 4: 16) ways, at 1 every tile above the mean load),
     then the frozen order reused (launches 4 and 5): every render equals the
     raster-ordered one bit for bit, counters included.  The first launch runs
     the order of the cold-frame cost probe (split too in the last case), the
@@ -247,10 +247,11 @@ def test_split_tiles_are_exact(rtc, monkeypatch, name, shard):
     rows = rtc.shard_rows(cam.height, shard[1])
     raster, s0 = _render_with_env(rtc, monkeypatch, {"RTC_TILE_ORDER": "0"}, scene, cam, "f32")
     raster = raster[:rows] if shard[1] == 1 else None
-    for split, most, probe in (("0.0001", "2", "8,24"), ("1", "2", "8,24"), ("0.0001", "3", "8,24,1")):
+    for split, most, probe in (("0.0001", "2", "8,24"), ("1", "2", "8,24"), ("0.0001", "3", "8,24,1"),
+                                 ("0.0001", "4", "8,24,1"), ("1", "4", "8,24")):
         monkeypatch.setenv("RTC_TILE_ORDER", "1")
         monkeypatch.setenv("RTC_SPLIT", split)
-        monkeypatch.setenv("RTC_SPLIT_MAX", most)  # up to 4 or 8 parts (half-wave seeds)
+        monkeypatch.setenv("RTC_SPLIT_MAX", most)  # up to 4, 8 (half-wave seeds) or 16 parts (wave-row seeds)
         monkeypatch.setenv("RTC_COLD_PROBE", probe)
         with rtc.Context(0) as c:
             c.upload(scene)
