@@ -134,10 +134,14 @@ struct rt_context {
     // 0.215 / 0.201 / 0.215 / 0.201, table 0.229 / 0.266 / 0.230 / 0.231.
     double urgent_factor = 0.125;
     bool urgent_graded = true;
-    // The first launch of a frame geometry orders its tiles by estimated
+    // RTC_COLD_PROBE=wr,wt[,split]: the first launch of a frame geometry orders its tiles by estimated
     // costs (probe_tiles: per sampled primary hit 1 + wr x reflective + wt x
-    // transparent), split by them if probe_split (RTC_COLD_PROBE=0 | wr,wt,split).
-    bool cold_probe = true;
+    // transparent), split by them if split is set.
+    // Off by default: same-box cold kernel ms, centre-out / probe (8,24):
+    // reflect_refract 0.455 / 0.51, refraction 0.42 / 0.49, cover 4K 1.17 /
+    // 1.20, table 4K 1.27 / 1.32, metal 0.090 / 0.112, cylinders 0.23 / 0.17
+    // (profiles/r03_cold_probe_sweep.txt).
+    bool cold_probe = false;
     float probe_wr = 8.0f, probe_wt = 24.0f;
     bool probe_split = false;
     int order_builds = 0;        // order_tiles runs for the current signature so far
