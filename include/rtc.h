@@ -279,6 +279,12 @@ int rt_debug_stamps(rt_context* ctx, uint64_t* out, uint32_t max_workgroups, uin
  * the largest pool launch so far, 0 before any). */
 int rt_debug_tile_costs(rt_context* ctx, uint32_t* out, uint32_t max_tiles, uint32_t* n);
 
+/* Diagnostics: the work items of the last pool launch made with
+ * RT_FLAG_STAMPS, in the order they were taken: 3 x u64 per item {item |
+ * workgroup << 32, start, end} (s_memrealtime, 100 MHz; item encoding in
+ * rtc_internal.hpp); *n = number of items logged. */
+int rt_debug_item_log(rt_context* ctx, uint64_t* out, uint32_t max_items, uint32_t* n);
+
 /* Known-answer harness: the device's own per-shape code for the shape at
  * world index `shape` of the uploaded world, on caller-given inputs (the
  * reference's per-shape unit tests, e.g. cone.rs:191-252, run on the GPU).

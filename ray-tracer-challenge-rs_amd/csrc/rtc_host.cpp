@@ -43,7 +43,8 @@ constexpr uint32_t kKindsSp = (1u << RT_SHAPE_SPHERE) | (1u << RT_SHAPE_PLANE);
 template <typename R>
 hipError_t launch_probe(const LaunchParams<R>& P, float wr, float wt, hipStream_t stream);
 hipError_t launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, uint32_t* n_items, float split_per_cost,
-                              uint32_t max_split_log2, float urgent_per_cost, uint32_t graded, hipStream_t stream);
+                              uint32_t max_split_log2, float urgent_per_cost, uint32_t graded, uint3 prio_cap,
+                              hipStream_t stream);
 template <typename R>
 hipError_t launch_debug_shape(const ShapeRec<R>* shapes, int slot, int kind, uint32_t mode, uint32_t world_space,
                               const double* in, uint32_t n, double* out, hipStream_t stream);
@@ -433,6 +434,13 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
 // from the previous frame's costs (scripts/camera_path.py), against 0.422
 // for a repeated camera; metal, whose 0.1 ms frames gain little from any
 // order, pays the 10 us sort (0.101 -> 0.107 ms).
+// Queue positions below which items may run at priority 3 / 2 / 1
+// (order_tiles): fractions of the resident grid (RTC_PRIO_CAP).
+uint3 prio_cap(const rt_context* ctx, uint32_t grid) {
+    auto at = [grid](double f) { return f > 0 ? (uint32_t)std::min(4e9, f * grid) : 0xFFFFFFFFu; };
+    return make_uint3(at(ctx->prio_cap[0]), at(ctx->prio_cap[1]), at(ctx->prio_cap[2]));
+}
+
 template <typename R>
 int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* cam, uint32_t depth, uint32_t grid,
                     hipStream_t stream) {
@@ -468,7 +476,7 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
         const float split = ctx->split_factor > 0 ? (float)(ctx->split_factor / grid) : 0.0f;
         const float urgent = ctx->urgent_factor > 0 ? (float)(ctx->urgent_factor / grid) : 0.0f;
         RT_HIP(launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, P.n_tiles, n_items, split, ctx->split_max,
-                                  urgent, ctx->urgent_graded, stream));
+                                  urgent, ctx->urgent_graded, prio_cap(ctx, grid), stream));
         ++ctx->order_builds;
         ctx->order_built = true;
     }
@@ -479,7 +487,7 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
         const float split = ctx->split_factor > 0 && ctx->probe_split ? (float)(ctx->split_factor / grid) : 0.0f;
         const float urgent = ctx->urgent_factor > 0 ? (float)(ctx->urgent_factor / grid) : 0.0f;
         RT_HIP(launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, P.n_tiles, n_items, split, ctx->split_max,
-                                  urgent, ctx->urgent_graded, stream));
+                                  urgent, ctx->urgent_graded, prio_cap(ctx, grid), stream));
         ctx->order_built = true;
     }
     if (ctx->order_built) {  // built from this frame's costs, or from the previous camera's frame
@@ -610,6 +618,18 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
         }
         P.stamps = ctx->d_stamps;
         ctx->stamp_count = ls.grid;
+        if (ls.pool) {  // every item of the launch: up to 2^kMaxSplitLog2 per tile
+            const size_t items = (size_t)P.n_tiles << kMaxSplitLog2;
+            if (ctx->item_log_capacity < items) {
+                (void)hipFree(ctx->d_item_log);
+                ctx->d_item_log = nullptr;
+                ctx->item_log_capacity = 0;
+                RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_item_log), (1 + 3 * items) * sizeof(uint64_t)));
+                ctx->item_log_capacity = items;
+            }
+            RT_HIP(hipMemsetAsync(ctx->d_item_log, 0, sizeof(uint64_t), stream));
+            P.item_log = ctx->d_item_log;
+        }
     }
     // Worlds of spheres and planes only run the pool kernel built without the
     // other kinds' loops (rtc_kernels_sp.o; same pixels).  Same-box A/B:
@@ -824,6 +844,11 @@ int create_device_context(int device_ordinal, rt_context** out) {
         if (n >= 3) ctx->probe_split = sp != 0;
     }
     if (const char* e = std::getenv("RTC_URGENT_GRADED")) ctx->urgent_graded = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("RTC_PRIO_CAP")) {  // 0 = none, or "f3,f2,f1" (fractions of the grid)
+        double f[3] = {0, 0, 0};
+        if (std::sscanf(e, "%lf,%lf,%lf", &f[0], &f[1], &f[2]) < 1) f[0] = 0;
+        for (int i = 0; i < 3; ++i) ctx->prio_cap[i] = f[0] > 0 ? f[i] : 0.0;
+    }
     if (const char* e = std::getenv("RTC_ORDER_BUILDS")) ctx->order_max_builds = std::atoi(e);
     if (const char* e = std::getenv("RTC_DIRECT_GRID")) ctx->direct_grid = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("RTC_JIT"))
@@ -855,6 +880,7 @@ void destroy_device_context(rt_context* ctx) {
     (void)hipFree(ctx->d_error);
     (void)hipFree(ctx->d_scratch);
     (void)hipFree(ctx->d_stamps);
+    (void)hipFree(ctx->d_item_log);
     (void)hipFree(ctx->d_spill);
     (void)hipFree(ctx->d_tile_cost);
     (void)hipFree(ctx->d_tile_order);
@@ -1148,6 +1174,19 @@ int rt_debug_stamps(rt_context* ctx, uint64_t* out, uint32_t max_wg, uint32_t* n
     const uint32_t copy = std::min(max_wg, ctx->stamp_count);
     if (out && copy)
         RT_HIP(hipMemcpy(out, ctx->d_stamps, 2 * sizeof(uint64_t) * copy, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_debug_item_log(rt_context* ctx, uint64_t* out, uint32_t max_items, uint32_t* n) {
+    if (!ctx || !n) return set_error(RT_ERR_INVALID, "null argument");
+    RT_HIP(hipSetDevice(ctx->device));
+    RT_HIP(hipDeviceSynchronize());
+    uint64_t count = 0;
+    if (ctx->d_item_log) RT_HIP(hipMemcpy(&count, ctx->d_item_log, sizeof count, hipMemcpyDeviceToHost));
+    *n = (uint32_t)std::min<uint64_t>(count, ctx->item_log_capacity);
+    const uint32_t copy = std::min(max_items, *n);
+    if (out && copy)
+        RT_HIP(hipMemcpy(out, ctx->d_item_log + 1, 3 * sizeof(uint64_t) * copy, hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

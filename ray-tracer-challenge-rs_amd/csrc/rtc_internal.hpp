@@ -213,6 +213,7 @@ struct LaunchParams {
     uint32_t world_lds;      // bytes of world tables staged at the start of dynamic LDS (0 = none)
     void* spill;                 // pool overflow: grid x 8 x (pool_capacity - pool_lds_capacity) words
     unsigned long long* stamps;  // RT_FLAG_STAMPS: 2 x grid s_memrealtime values
+    unsigned long long* item_log;  // RT_FLAG_STAMPS pool launches: [0] count, then 3 x u64 per item
     unsigned long long* tile_counter;  // kTileQueues queue heads, kQueueStride apart (zero at launch)
     unsigned long long* next_tile_counter;  // the heads of the next dynamic launch, zeroed by this one
     const uint32_t* tile_order;        // queue position -> work item (heaviest first), null = raster order

@@ -1710,6 +1710,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
             if (split) atomicMax(&P.tile_cost[t], c << split);
             else P.tile_cost[t] = c;
         }
+        if (tid == 0 && P.item_log) {  // diagnostics (RT_FLAG_STAMPS): the item's span
+            const unsigned long long k = atomicAdd(&P.item_log[0], 1ull);
+            P.item_log[1 + 3 * k] = item | (unsigned long long)blockIdx.x << 32;
+            P.item_log[2 + 3 * k] = tile_start;
+            P.item_log[3 + 3 * k] = __builtin_amdgcn_s_memrealtime();
+        }
     }
     if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
     if (P.stamps) {
@@ -1793,7 +1799,7 @@ __global__ __launch_bounds__(kOrderThreads) void order_tiles(uint32_t* __restric
                                                              uint32_t* __restrict__ order, uint32_t n,
                                                              uint32_t* __restrict__ n_items, float split_per_cost,
                                                              uint32_t max_log2, float urgent_per_cost,
-                                                             uint32_t graded) {
+                                                             uint32_t graded, uint3 prio_cap) {
     __shared__ uint32_t hist[kOrderBuckets];
     __shared__ uint32_t scan[kOrderBuckets];
     __shared__ unsigned long long total;
@@ -1851,9 +1857,13 @@ __global__ __launch_bounds__(kOrderThreads) void order_tiles(uint32_t* __restric
         // priority: 3 above the urgent cost, or graded 1/2/3 above 1x/2x/4x it
         const float pc = (float)(c >> l);
         const uint32_t pr = !(pc > urgent) ? 0u : !graded ? 3u : pc > 4.0f * urgent ? 3u : pc > 2.0f * urgent ? 2u : 1u;
-        const uint32_t flag = pr << kItemPrioShift;
-        for (uint32_t p = 0; p < (1u << l); ++p)
-            order[pos + p] = i | p << kItemPartShift | l << kItemSplitShift | flag;
+        for (uint32_t p = 0; p < (1u << l); ++p) {
+            // at most prio_cap.x items at priority 3, .y at 2 or more, .z at 1 or more
+            // (queue positions: the first ones are taken first, about one per CU)
+            const uint32_t q = pos + p;
+            const uint32_t cap = q < prio_cap.x ? 3u : q < prio_cap.y ? 2u : q < prio_cap.z ? 1u : 0u;
+            order[q] = i | p << kItemPartShift | l << kItemSplitShift | min(pr, cap) << kItemPrioShift;
+        }
         if (l) cost[i] = 0;
     }
     if (threadIdx.x == 0) *n_items = items;
@@ -1989,10 +1999,11 @@ template hipError_t occupancy<double>(bool, bool, size_t, int*);
 
 #if RTC_PRECISION != 2
 hipError_t launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, uint32_t* n_items, float split_per_cost,
-                              uint32_t max_split_log2, float urgent_per_cost, uint32_t graded, hipStream_t stream) {
+                              uint32_t max_split_log2, float urgent_per_cost, uint32_t graded, uint3 prio_cap,
+                              hipStream_t stream) {
     (void)hipGetLastError();  // see launch_trace
     hipLaunchKernelGGL(order_tiles, dim3(1), dim3(kOrderThreads), 0, stream, cost, order, n, n_items, split_per_cost,
-                       max_split_log2, urgent_per_cost, graded);
+                       max_split_log2, urgent_per_cost, graded, prio_cap);
     return hipGetLastError();
 }
 #endif

@@ -162,6 +162,7 @@ def _load() -> C.CDLL:
         "rt_read_counters": (C.c_int, [C.c_void_p, P(Stats)]),
         "rt_debug_stamps": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_uint32, P(C.c_uint32)]),
         "rt_debug_tile_costs": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_uint32, P(C.c_uint32)]),
+        "rt_debug_item_log": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_uint32, P(C.c_uint32)]),
         "rt_assemble_shards": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                          C.c_void_p, C.c_void_p]),
         "rt_scene_load_yaml": (C.c_int, [C.c_char_p, P(C.c_void_p)]),
@@ -204,7 +205,7 @@ _lib = _load()
 EXPORTED_SYMBOLS = (
     "rt_abi_version", "rt_last_error", "rt_device_count", "rt_context_create", "rt_context_destroy",
     "rt_scene_upload", "rt_shard_rows", "rt_render", "rt_render_device", "rt_color_at", "rt_read_counters",
-    "rt_debug_stamps", "rt_debug_tile_costs", "rt_debug_intersect", "rt_debug_normal", "rt_camera_set_transform",
+    "rt_debug_stamps", "rt_debug_tile_costs", "rt_debug_item_log", "rt_debug_intersect", "rt_debug_normal", "rt_camera_set_transform",
     "rt_shard_row_map", "rt_context_create_multi", "rt_comm_unique_id", "rt_context_create_rank", "rt_context_group",
     "rt_context_set_jit", "rt_jit_status", "rt_jit_wait",
     "rt_assemble_shards", "rt_scene_load_yaml", "rt_scene_load_yaml_text", "rt_scene_view_get", "rt_scene_free",
@@ -493,6 +494,14 @@ class Context:
         _check(_lib.rt_debug_stamps(self._h, None, 0, C.byref(n)))
         out = np.zeros((n.value, 2), dtype=np.uint64)
         _check(_lib.rt_debug_stamps(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), n.value, C.byref(n)))
+        return out
+
+    def debug_item_log(self) -> np.ndarray:
+        """Items of the last RT_FLAG_STAMPS pool launch: rows {item | wg << 32, start, end}."""
+        n = C.c_uint32()
+        _check(_lib.rt_debug_item_log(self._h, None, 0, C.byref(n)))
+        out = np.zeros((n.value, 3), dtype=np.uint64)
+        _check(_lib.rt_debug_item_log(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), n.value, C.byref(n)))
         return out
 
     def debug_tile_costs(self) -> np.ndarray:

@@ -60,4 +60,23 @@ with rtc_amd.Context(0) as ctx:
         # how many workgroups are still running at each time: the tail's width
         grid_t = np.linspace(0, end.max(), 21)
         res["running_at_5pct_steps"] = [int(((start <= t) & (end > t)).sum()) for t in grid_t]
+        log = ctx.debug_item_log().astype(np.int64)
+        if len(log):
+            item, wg = log[:, 0] & 0xFFFFFFFF, log[:, 0] >> 32
+            s0, e0 = (log[:, 1] - t0) * 1e-2, (log[:, 2] - t0) * 1e-2
+            dur = e0 - s0
+            split, prio = (item >> 24) & 7, (item >> 27) & 3
+            last = np.argsort(e0)[::-1][:12]
+            res["items"] = int(len(log))
+            res["item_dur_q_us"] = q(dur)
+            res["items_by_split"] = np.bincount(split, minlength=4).tolist()
+            res["items_by_prio"] = np.bincount(prio, minlength=4).tolist()
+            res["last_items"] = [{"start": round(float(s0[i]), 1), "dur": round(float(dur[i]), 1), "split": int(split[i]),
+                                  "prio": int(prio[i]), "wg_items": int((wg == wg[i]).sum())} for i in last]
+            longest = np.argsort(dur)[::-1][:8]
+            res["longest_items"] = [{"start": round(float(s0[i]), 1), "dur": round(float(dur[i]), 1), "split": int(split[i]),
+                                     "prio": int(prio[i])} for i in longest]
+            late = s0 > 0.5 * end.max()
+            res["items_started_after_half_span"] = int(late.sum())
+            res["late_item_dur_q_us"] = q(dur[late]) if late.any() else None
         print(json.dumps(res), flush=True)
