@@ -134,10 +134,6 @@ struct rt_context {
     // 0.215 / 0.201 / 0.215 / 0.201, table 0.229 / 0.266 / 0.230 / 0.231.
     double urgent_factor = 0.125;
     bool urgent_graded = true;
-    // ... and only the first prio_cap[0] x grid queue positions at 3,
-    // prio_cap[1] x grid at 2 or more, prio_cap[2] x grid at 1 or more (0 = no cap;
-    // RTC_PRIO_CAP=f3,f2,f1).
-    double prio_cap[3] = {0, 0, 0};
     // RTC_COLD_PROBE=wr,wt[,split]: the first launch of a frame geometry orders its tiles by estimated
     // costs (probe_tiles: per sampled primary hit 1 + wr x reflective + wt x
     // transparent), split by them if split is set.

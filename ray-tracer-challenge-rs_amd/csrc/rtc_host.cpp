@@ -43,8 +43,7 @@ constexpr uint32_t kKindsSp = (1u << RT_SHAPE_SPHERE) | (1u << RT_SHAPE_PLANE);
 template <typename R>
 hipError_t launch_probe(const LaunchParams<R>& P, float wr, float wt, hipStream_t stream);
 hipError_t launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, uint32_t* n_items, float split_per_cost,
-                              uint32_t max_split_log2, float urgent_per_cost, uint32_t graded, uint3 prio_cap,
-                              hipStream_t stream);
+                              uint32_t max_split_log2, float urgent_per_cost, uint32_t graded, hipStream_t stream);
 template <typename R>
 hipError_t launch_debug_shape(const ShapeRec<R>* shapes, int slot, int kind, uint32_t mode, uint32_t world_space,
                               const double* in, uint32_t n, double* out, hipStream_t stream);
@@ -295,13 +294,11 @@ uint32_t tile_rows_for(uint32_t height, uint32_t shards, uint32_t shard) {
 }
 
 // Rays held by the LDS pool for a given depth and pop batch (LIFO bound).
-// (RTC_OVERLAP: the next item's seeds land on a pool of fewer than a batch of
-// the previous item's rays)
-uint32_t pool_capacity(uint32_t depth, uint32_t batch) { return (uint32_t)kBlock * kAccSlots + depth * batch; }
+uint32_t pool_capacity(uint32_t depth, uint32_t batch) { return (uint32_t)kBlock + depth * batch; }
 
 template <typename R>
 size_t pool_lds_bytes(uint32_t cap) {
-    return kAccSlots * 3 * kBlock * sizeof(long long) + (size_t)cap * (7 * sizeof(R) + sizeof(uint32_t));
+    return 3 * kBlock * sizeof(long long) + (size_t)cap * (7 * sizeof(R) + sizeof(uint32_t));
 }
 
 constexpr size_t kLdsPerCu = 160 * 1024;
@@ -434,13 +431,6 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
 // from the previous frame's costs (scripts/camera_path.py), against 0.422
 // for a repeated camera; metal, whose 0.1 ms frames gain little from any
 // order, pays the 10 us sort (0.101 -> 0.107 ms).
-// Queue positions below which items may run at priority 3 / 2 / 1
-// (order_tiles): fractions of the resident grid (RTC_PRIO_CAP).
-uint3 prio_cap(const rt_context* ctx, uint32_t grid) {
-    auto at = [grid](double f) { return f > 0 ? (uint32_t)std::min(4e9, f * grid) : 0xFFFFFFFFu; };
-    return make_uint3(at(ctx->prio_cap[0]), at(ctx->prio_cap[1]), at(ctx->prio_cap[2]));
-}
-
 template <typename R>
 int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* cam, uint32_t depth, uint32_t grid,
                     hipStream_t stream) {
@@ -476,7 +466,7 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
         const float split = ctx->split_factor > 0 ? (float)(ctx->split_factor / grid) : 0.0f;
         const float urgent = ctx->urgent_factor > 0 ? (float)(ctx->urgent_factor / grid) : 0.0f;
         RT_HIP(launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, P.n_tiles, n_items, split, ctx->split_max,
-                                  urgent, ctx->urgent_graded, prio_cap(ctx, grid), stream));
+                                  urgent, ctx->urgent_graded, stream));
         ++ctx->order_builds;
         ctx->order_built = true;
     }
@@ -487,7 +477,7 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
         const float split = ctx->split_factor > 0 && ctx->probe_split ? (float)(ctx->split_factor / grid) : 0.0f;
         const float urgent = ctx->urgent_factor > 0 ? (float)(ctx->urgent_factor / grid) : 0.0f;
         RT_HIP(launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, P.n_tiles, n_items, split, ctx->split_max,
-                                  urgent, ctx->urgent_graded, prio_cap(ctx, grid), stream));
+                                  urgent, ctx->urgent_graded, stream));
         ctx->order_built = true;
     }
     if (ctx->order_built) {  // built from this frame's costs, or from the previous camera's frame
@@ -844,11 +834,6 @@ int create_device_context(int device_ordinal, rt_context** out) {
         if (n >= 3) ctx->probe_split = sp != 0;
     }
     if (const char* e = std::getenv("RTC_URGENT_GRADED")) ctx->urgent_graded = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("RTC_PRIO_CAP")) {  // 0 = none, or "f3,f2,f1" (fractions of the grid)
-        double f[3] = {0, 0, 0};
-        if (std::sscanf(e, "%lf,%lf,%lf", &f[0], &f[1], &f[2]) < 1) f[0] = 0;
-        for (int i = 0; i < 3; ++i) ctx->prio_cap[i] = f[0] > 0 ? f[i] : 0.0;
-    }
     if (const char* e = std::getenv("RTC_ORDER_BUILDS")) ctx->order_max_builds = std::atoi(e);
     if (const char* e = std::getenv("RTC_DIRECT_GRID")) ctx->direct_grid = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("RTC_JIT"))

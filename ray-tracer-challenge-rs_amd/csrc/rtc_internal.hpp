@@ -81,11 +81,6 @@ constexpr int kQueueStride = 32;
 constexpr uint32_t kItemTileMask = 0xFFFFFu;
 constexpr uint32_t kItemPartShift = 20, kItemSplitShift = 24, kItemPartMask = 15u, kItemSplitMask = 7u;
 constexpr uint32_t kItemPrioShift = 27;
-// Pool kernel with two items' rays in flight at once (trace_pool): 2 accumulator slots.
-#ifndef RTC_OVERLAP
-#define RTC_OVERLAP 0
-#endif
-constexpr uint32_t kAccSlots = RTC_OVERLAP ? 2 : 1;
 constexpr uint32_t kMaxSplitLog2 = 4;  // up to 16 items per tile
 // Tile scheduling modes (RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic)
 constexpr uint32_t kSchedGrid = 0;     // one workgroup per tile; the dispatcher balances

@@ -1409,199 +1409,6 @@ __device__ inline void acc_add(long long* acc, uint32_t pix, double v) {
     if (q) atomicAdd(reinterpret_cast<unsigned long long*>(&acc[pix]), (unsigned long long)q);
 }
 
-#if RTC_OVERLAP
-// This item's pixel of thread tid: validity (the item's part of the tile) and
-// output index, as load_primary and the part mask give them.
-template <typename R>
-__device__ inline bool item_pixel(const LaunchParams<R>& P, uint32_t item, uint32_t tid, uint64_t& out_idx) {
-    const uint32_t t = item & kItemTileMask, split = (item >> kItemSplitShift) & kItemSplitMask;
-    bool valid;
-    if (P.rays) {
-        const uint64_t r = (uint64_t)t * kBlock + tid;
-        valid = r < P.n_rays;
-        out_idx = r;
-    } else {
-        uint32_t x, y;
-        valid = tile_pixel(P, t, tid, x, y, out_idx);
-    }
-    return valid && (tid >> (8 - split)) == ((item >> kItemPartShift) & kItemPartMask);
-}
-
-// Overlapped items (RTC_OVERLAP): the pool holds the rays of up to two items
-// at once (accumulator slot in meta bit 31).  The next item is admitted as
-// soon as a slot is free and the pool holds fewer rays than a pop batch (the
-// lanes would idle), so one item's last, thin generations run together with
-// the next one's first.  An item is written out when its live-ray count (rays
-// pushed and not yet shaded) reaches zero.
-template <typename R, bool kLds, bool kDup>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 4 ? RTC_POOL_WAVES : 1))) void trace_pool(
-    LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
-    extern __shared__ __align__(16) unsigned char smem_all[];
-    const DevScene<R> sc = scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem_all, true);
-    if (P.stamps && threadIdx.x == 0) P.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-    unsigned char* smem = smem_all + (kLds ? P.world_lds : 0);
-    constexpr uint32_t kNone = 0xFFFFFFFFu, kSlotBit = 1u << 31;
-    __shared__ unsigned int s_item[2];  // the item in accumulator slot s (kNone: free)
-    __shared__ int s_live[2];           // its rays pushed and not yet shaded
-    __shared__ unsigned int s_new;
-    __shared__ int s_top[2];
-    const uint32_t cap = P.pool_capacity;
-    const uint32_t lcap = P.pool_lds_capacity, gcap = cap - lcap;
-    Pool<R> pl;
-    pl.acc = reinterpret_cast<long long*>(smem);  // 2 slots x 3 x kBlock
-    pl.lds = reinterpret_cast<R*>(smem + 6 * kBlock * sizeof(long long));
-    pl.lds_cap = (int)lcap;
-    pl.spill = reinterpret_cast<R*>(P.spill) + (size_t)blockIdx.x * 8 * gcap;
-    pl.spill_cap = (int)gcap;
-
-    Counts k = {};
-    const uint32_t tid = threadIdx.x;
-    if (P.persistent == kSchedDynamic && blockIdx.x == 0 && tid < (uint32_t)kTileQueues)
-        P.next_tile_counter[tid * kQueueStride] = 0ull;
-    uint32_t probe = 0, it = 0;
-    const uint32_t n_items = P.item_count && tid == 0 ? *P.item_count : P.n_tiles;
-    unsigned long long start0 = 0, start1 = 0;  // thread 0: each slot's admission time
-    for (int c = 0; c < 6; ++c) pl.acc[c * kBlock + tid] = 0;
-    if (tid < 2) {
-        s_item[tid] = kNone;
-        s_live[tid] = 0;
-        s_top[tid] = 0;
-    }
-    __syncthreads();
-    bool drained = false;
-    for (uint32_t gen = 0;; ++gen) {
-        const int cur = gen & 1;
-        int size = s_top[cur];
-        const uint32_t it0 = __builtin_amdgcn_readfirstlane(s_item[0]), it1 = __builtin_amdgcn_readfirstlane(s_item[1]);
-        const int free_slot = it0 == kNone ? 0 : (it1 == kNone ? 1 : -1);
-        if (!drained && free_slot >= 0 && size < (int)P.pop_batch) {
-            if (tid == 0) {
-                s_new = next_tile(P, it, probe, n_items);
-                if (free_slot) start1 = __builtin_amdgcn_s_memrealtime();
-                else start0 = __builtin_amdgcn_s_memrealtime();
-            }
-            ++it;
-            __syncthreads();
-            const uint32_t item = __builtin_amdgcn_readfirstlane(s_new);
-            if (item == kNone) {
-                drained = true;
-            } else {
-                bool valid;
-                V3<R> o, d;
-                uint64_t out_idx;
-                load_primary(P, item & kItemTileMask, tid, valid, o, d, out_idx);
-                const uint32_t split = (item >> kItemSplitShift) & kItemSplitMask;
-                valid &= (tid >> (8 - split)) == ((item >> kItemPartShift) & kItemPartMask);
-                k.c[0] += wave_count(valid);
-                const int slot = wave_reserve(valid, &s_top[cur]);
-                if (valid) pool_put(pl, slot, o, d, (R)1, tid | (P.max_depth << 8) | (free_slot ? kSlotBit : 0u));
-                __syncthreads();
-                if (tid == 0) {
-                    s_live[free_slot] = s_top[cur] - size;
-                    s_item[free_slot] = item;
-                }
-                const uint32_t other = free_slot ? it0 : it1;
-                const uint32_t pa = (item >> kItemPrioShift) & 3u, pb = other == kNone ? 0u : (other >> kItemPrioShift) & 3u;
-                set_wave_prio(pa > pb ? pa : pb);
-            }
-            __syncthreads();
-            size = s_top[cur];
-        }
-        if (size == 0 && drained) break;
-        if (gen >= (1u << 24)) {  // no workgroup runs this long: a live count lost track, stop (error)
-            if (tid == 0) atomicOr(P.error_flag, 2);
-            break;
-        }
-        if (size > 0) {
-            const int kpop = size < (int)P.pop_batch ? size : (int)P.pop_batch;
-            const int bottom = size - kpop;
-            const bool active = (int)tid < kpop;
-            V3<R> ro, rd;
-            R rw = (R)0;
-            uint32_t meta = 0;
-            if (active) pool_get(pl, bottom + (int)tid, ro, rd, rw, meta);
-            if (tid == 0) s_top[cur ^ 1] = bottom;
-            __syncthreads();
-            Shaded<R> sh;
-            bool hit = false;
-            const uint32_t pix = meta & 0xFFu, rem = (meta >> 8) & 0x7FFFFFu, sbit = meta & kSlotBit;
-            const uint32_t child_meta = pix | ((rem - 1u) << 8) | sbit;
-            auto push = [&](V3<R> co, V3<R> cd, R cw) {
-                const int slot = wave_reserve(true, &s_top[cur ^ 1]);
-                if (slot < (int)cap) pool_put(pl, slot, co, cd, rw * cw, child_meta);
-                else atomicOr(P.error_flag, 1);
-            };
-            if (active) hit = shade_ray<R, true, kDup>(sc, ro, rd, rem, sh, push);
-            count_events(k, false, hit, sh, sc.n_lights);
-            if (hit) {
-                long long* acc = pl.acc + (sbit ? 3 * kBlock : 0);
-                acc_add(acc, pix, (double)(sh.surface.x * rw));
-                acc_add(acc + kBlock, pix, (double)(sh.surface.y * rw));
-                acc_add(acc + 2 * kBlock, pix, (double)(sh.surface.z * rw));
-            }
-            // live rays per slot: + children - the shaded ray (one LDS atomic per wave and slot)
-            const bool s1 = sbit != 0;
-            const int d0 = (int)wave_count(hit & !s1 & sh.refl_child) + (int)wave_count(hit & !s1 & sh.refr_child) -
-                           (int)wave_count(active & !s1);
-            const int d1 = (int)wave_count(hit & s1 & sh.refl_child) + (int)wave_count(hit & s1 & sh.refr_child) -
-                           (int)wave_count(active & s1);
-            if ((tid & 63) == 0) {
-                if (d0) atomicAdd(&s_live[0], d0);
-                if (d1) atomicAdd(&s_live[1], d1);
-            }
-            __syncthreads();  // pushes and counts complete
-            if (s_top[cur ^ 1] > (int)cap) {  // overflowed: drop the pool and both items' rays (error flagged)
-                __syncthreads();
-                if (tid == 0) {
-                    s_top[cur ^ 1] = 0;
-                    s_live[0] = s_live[1] = 0;
-                }
-                __syncthreads();
-            }
-        } else {
-            if (tid == 0) s_top[cur ^ 1] = 0;
-            __syncthreads();
-        }
-        // write out the items whose rays are all shaded
-        const uint32_t a0 = __builtin_amdgcn_readfirstlane(s_item[0]), a1 = __builtin_amdgcn_readfirstlane(s_item[1]);
-        const bool done0 = a0 != kNone && __builtin_amdgcn_readfirstlane(s_live[0]) == 0;
-        const bool done1 = a1 != kNone && __builtin_amdgcn_readfirstlane(s_live[1]) == 0;
-        if (done0 | done1) {
-            for (int s = 0; s < 2; ++s) {
-                if (!(s ? done1 : done0)) continue;
-                const uint32_t item = s ? a1 : a0;
-                long long* acc = pl.acc + s * 3 * kBlock;
-                uint64_t out_idx;
-                if (item_pixel(P, item, tid, out_idx))
-                    store_pixel(P, out_idx, V3<R>{(R)((double)acc[tid] * kAccInvScale),
-                                                  (R)((double)acc[kBlock + tid] * kAccInvScale),
-                                                  (R)((double)acc[2 * kBlock + tid] * kAccInvScale)});
-                acc[tid] = acc[kBlock + tid] = acc[2 * kBlock + tid] = 0;
-                if (tid == 0) {
-                    if (P.tile_cost) {
-                        const uint32_t t = item & kItemTileMask, split = (item >> kItemSplitShift) & kItemSplitMask;
-                        const uint32_t c =
-                            (uint32_t)min(__builtin_amdgcn_s_memrealtime() - (s ? start1 : start0), 0x0FFFFFFFull);
-                        if (split) atomicMax(&P.tile_cost[t], c << split);
-                        else P.tile_cost[t] = c;
-                    }
-                    s_item[s] = kNone;
-                }
-            }
-            const uint32_t r0 = done0 ? kNone : a0, r1 = done1 ? kNone : a1;
-            const uint32_t pa = r0 == kNone ? 0u : (r0 >> kItemPrioShift) & 3u;
-            const uint32_t pb = r1 == kNone ? 0u : (r1 >> kItemPrioShift) & 3u;
-            set_wave_prio(pa > pb ? pa : pb);
-            __syncthreads();
-        }
-    }
-    if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
-    if (P.stamps) {
-        __syncthreads();
-        if (threadIdx.x == 0) P.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-    }
-}
-#else
 template <typename R, bool kLds, bool kDup>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 4 ? RTC_POOL_WAVES : 1))) void trace_pool(
     LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
@@ -1723,7 +1530,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         if (threadIdx.x == 0) P.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
     }
 }
-#endif  // RTC_OVERLAP
 
 // Tile-cost estimate for a frame with no recorded costs (its first launch):
 // kProbeSamples primary rays per tile, each charged 1 + wr x [reflective] +
@@ -1799,7 +1605,7 @@ __global__ __launch_bounds__(kOrderThreads) void order_tiles(uint32_t* __restric
                                                              uint32_t* __restrict__ order, uint32_t n,
                                                              uint32_t* __restrict__ n_items, float split_per_cost,
                                                              uint32_t max_log2, float urgent_per_cost,
-                                                             uint32_t graded, uint3 prio_cap) {
+                                                             uint32_t graded) {
     __shared__ uint32_t hist[kOrderBuckets];
     __shared__ uint32_t scan[kOrderBuckets];
     __shared__ unsigned long long total;
@@ -1857,13 +1663,9 @@ __global__ __launch_bounds__(kOrderThreads) void order_tiles(uint32_t* __restric
         // priority: 3 above the urgent cost, or graded 1/2/3 above 1x/2x/4x it
         const float pc = (float)(c >> l);
         const uint32_t pr = !(pc > urgent) ? 0u : !graded ? 3u : pc > 4.0f * urgent ? 3u : pc > 2.0f * urgent ? 2u : 1u;
-        for (uint32_t p = 0; p < (1u << l); ++p) {
-            // at most prio_cap.x items at priority 3, .y at 2 or more, .z at 1 or more
-            // (queue positions: the first ones are taken first, about one per CU)
-            const uint32_t q = pos + p;
-            const uint32_t cap = q < prio_cap.x ? 3u : q < prio_cap.y ? 2u : q < prio_cap.z ? 1u : 0u;
-            order[q] = i | p << kItemPartShift | l << kItemSplitShift | min(pr, cap) << kItemPrioShift;
-        }
+        const uint32_t flag = pr << kItemPrioShift;
+        for (uint32_t p = 0; p < (1u << l); ++p)
+            order[pos + p] = i | p << kItemPartShift | l << kItemSplitShift | flag;
         if (l) cost[i] = 0;
     }
     if (threadIdx.x == 0) *n_items = items;
@@ -1999,11 +1801,10 @@ template hipError_t occupancy<double>(bool, bool, size_t, int*);
 
 #if RTC_PRECISION != 2
 hipError_t launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, uint32_t* n_items, float split_per_cost,
-                              uint32_t max_split_log2, float urgent_per_cost, uint32_t graded, uint3 prio_cap,
-                              hipStream_t stream) {
+                              uint32_t max_split_log2, float urgent_per_cost, uint32_t graded, hipStream_t stream) {
     (void)hipGetLastError();  // see launch_trace
     hipLaunchKernelGGL(order_tiles, dim3(1), dim3(kOrderThreads), 0, stream, cost, order, n, n_items, split_per_cost,
-                       max_split_log2, urgent_per_cost, graded, prio_cap);
+                       max_split_log2, urgent_per_cost, graded);
     return hipGetLastError();
 }
 #endif
