@@ -1085,10 +1085,14 @@ __device__ inline bool tile_pixel(const LaunchParams<R>& P, uint32_t t, uint32_t
     return x < P.width && y < P.height;
 }
 
-template <typename R>
+// kFramesOnly: the caller never runs in color_at mode (per-scene direct
+// kernels, rtc_host.cpp launch: camera frames only).  Same-box A/B: three_sphere
+// 1080p 19.9 -> 19.4 us, shadow_puppets -1.6 %; the per-scene pool kernel
+// lost 1-2 % that way (register allocation) and keeps the branch.
+template <typename R, bool kFramesOnly = false>
 __device__ inline void load_primary(const LaunchParams<R>& P, uint32_t t, uint32_t tid, bool& valid, V3<R>& o,
                                     V3<R>& d, uint64_t& out_idx) {
-    if (P.rays) {  // color_at mode: tile = 256 consecutive rays
+    if (!kFramesOnly && P.rays) {  // color_at mode: tile = 256 consecutive rays
         const uint64_t r = (uint64_t)t * kBlock + tid;
         valid = r < P.n_rays;
         out_idx = r;
@@ -1253,7 +1257,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         bool valid;
         V3<R> o, d;
         uint64_t out_idx;
+#ifdef RTC_JIT
+        load_primary<R, true>(P, t, tid, valid, o, d, out_idx);
+#else
         load_primary(P, t, tid, valid, o, d, out_idx);
+#endif
         V3<R> c = {(R)0, (R)0, (R)0};
         Shaded<R> sh;
         bool hit = false;
