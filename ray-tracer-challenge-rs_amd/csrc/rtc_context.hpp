@@ -161,6 +161,8 @@ struct rt_context {
     // RTC_JIT / rt_context_set_jit = RT_JIT_OFF | RT_JIT_SYNC | RT_JIT_AUTO
     // (default) | RT_JIT_EAGER (rtc.h).
     std::vector<rtc::ShapeRec<float>> jit_shapes;
+    std::vector<rtc::LightRec<float>> jit_lights;  // per-scene builds unroll the lights as constants
+    bool jit_patterns = true;                      // some material has a pattern (else pattern code is dropped)
     int32_t jit_begin[rtc::kNumKinds + 1] = {};
     hipFunction_t jit_fn[4] = {};
     std::shared_ptr<rtc::CodeBuild> jit_build[4];  // the build each variant waits for (host thread)

@@ -637,7 +637,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     // large f32 frames run the per-scene build of the same kernel (rtc_jit.cpp)
     hipFunction_t jf = nullptr;
     if constexpr (sizeof(R) == 4) {
-        const bool want = cam && !dup && !(flags & RT_FLAG_STAMPS) &&
+        const bool want = cam && !dup && !(flags & (RT_FLAG_STAMPS | RT_FLAG_NO_SHADE | RT_FLAG_NO_TRACE)) &&
                           (ctx->jit_mode == RT_JIT_SYNC || (ctx->jit_mode >= RT_JIT_AUTO && P.n_tiles >= kJitMinTiles));
         if (want) ++ctx->jit_frames;
         if (want && (rc = jit_function(ctx, ls.pool, ls.world_lds != 0, ls.lds, ls.per_cu, &jf))) return rc;
@@ -928,6 +928,12 @@ int capture_jit_table(rt_context* ctx) {
     ctx->jit_shapes.assign(n, ShapeRec<float>{});
     if (n) RT_HIP(hipMemcpy(ctx->jit_shapes.data(), ctx->w32.shapes, n * sizeof(ShapeRec<float>), hipMemcpyDeviceToHost));
     for (int k = 0; k <= kNumKinds; ++k) ctx->jit_begin[k] = ctx->w32.scene.kind_begin[k];
+    const int32_t nl = ctx->w32.scene.n_lights, nm = ctx->w32.scene.n_materials;
+    ctx->jit_lights.assign(nl, LightRec<float>{});
+    if (nl) RT_HIP(hipMemcpy(ctx->jit_lights.data(), ctx->w32.lights, nl * sizeof(LightRec<float>), hipMemcpyDeviceToHost));
+    std::vector<MaterialRec<float>> mats(nm);
+    if (nm) RT_HIP(hipMemcpy(mats.data(), ctx->w32.materials, nm * sizeof(MaterialRec<float>), hipMemcpyDeviceToHost));
+    ctx->jit_patterns = std::any_of(mats.begin(), mats.end(), [](const MaterialRec<float>& m) { return m.pattern >= 0; });
     for (int v = 0; v < 4; ++v) {
         ctx->jit_fn[v] = nullptr;
         ctx->jit_build[v].reset();

@@ -92,8 +92,10 @@ std::string floats(const float (&a)[N]) {
     return s + "}";
 }
 
-// rtc_jit_scene.hpp: the world's f32 shape table as constexpr data.
-std::string scene_header(const std::vector<ShapeRec<float>>& sh, const int32_t begin[kNumKinds + 1]) {
+// rtc_jit_scene.hpp: the world's f32 shape table, its lights and whether any
+// material has a pattern, as constexpr data.
+std::string scene_header(const std::vector<ShapeRec<float>>& sh, const int32_t begin[kNumKinds + 1],
+                         const std::vector<LightRec<float>>& lights, bool patterns) {
     std::string s = "#pragma once\n#include \"rtc_internal.hpp\"\nnamespace rtc {\nnamespace jit {\n";
     s += "constexpr int kBegin[" + std::to_string(kNumKinds + 1) + "] = {";
     for (int k = 0; k <= kNumKinds; ++k) s += (k ? ", " : "") + std::to_string(begin[k]);
@@ -103,7 +105,13 @@ std::string scene_header(const std::vector<ShapeRec<float>>& sh, const int32_t b
              std::to_string(r.casts_shadow) + ", " + std::to_string(r.material) + ", " + std::to_string(r.flags) +
              ", " + hexf(r.ymin) + ", " + hexf(r.ymax) + ", " + floats(r.tri) + "},\n";
     }
-    s += "    {}};\n}  // namespace jit\n}  // namespace rtc\n";
+    s += "    {}};\n";
+    s += "constexpr int kNumLights = " + std::to_string(lights.size()) + ";\n";
+    s += "constexpr LightRec<float> kLights[" + std::to_string(lights.size() + 1) + "] = {\n";
+    for (const LightRec<float>& l : lights) s += "    {" + floats(l.position) + ", " + floats(l.intensity) + "},\n";
+    s += "    {}};\n";
+    s += std::string("constexpr bool kPatterns = ") + (patterns ? "true" : "false") + ";\n";
+    s += "}  // namespace jit\n}  // namespace rtc\n";
     return s;
 }
 
@@ -364,8 +372,10 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
     const bool sync = ctx->jit_mode == RT_JIT_SYNC;
     std::shared_ptr<CodeBuild>& b = ctx->jit_build[variant];
     if (!b) {
-        const uint64_t table = fnv(ctx->jit_begin, sizeof ctx->jit_begin,
-                                   fnv(ctx->jit_shapes.data(), ctx->jit_shapes.size() * sizeof(ShapeRec<float>)));
+        uint64_t table = fnv(ctx->jit_begin, sizeof ctx->jit_begin,
+                             fnv(ctx->jit_shapes.data(), ctx->jit_shapes.size() * sizeof(ShapeRec<float>)));
+        table = fnv(ctx->jit_lights.data(), ctx->jit_lights.size() * sizeof(LightRec<float>), table);
+        table = fnv(&ctx->jit_patterns, sizeof ctx->jit_patterns, table);
         const uint32_t start_at = ctx->jit_mode == RT_JIT_AUTO ? 2 : 1;
         bool start = false;
         {
@@ -384,7 +394,8 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
             ctx->jit_owner[variant] = true;
             uint64_t key = 0;
             const jitfile::Request rq =
-                make_request(scene_header(ctx->jit_shapes, ctx->jit_begin), kernel_name(pool, lds), ctx->arch, &key);
+                make_request(scene_header(ctx->jit_shapes, ctx->jit_begin, ctx->jit_lights, ctx->jit_patterns),
+                             kernel_name(pool, lds), ctx->arch, &key);
             start_build(b, rq, key, sync);
         }
     }

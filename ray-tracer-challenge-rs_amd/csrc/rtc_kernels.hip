@@ -922,8 +922,36 @@ __device__ inline const MaterialRec<R>& prepare_hit(const DevScene<R>& sc, V3<R>
     q.over = along(q.p, q.n, Real<R>::surface_offset(q.p.x, q.p.y, q.p.z));
     q.base = {m.color[0], m.color[1], m.color[2]};
     patterned = m.pattern >= 0;
-    if (patterned) q.base = pattern_color(sc, m.pattern, s, q.over);
+#ifdef RTC_JIT
+    constexpr bool kPatterns = jit::kPatterns;  // per-scene build: no pattern in the world, no pattern code
+#else
+    constexpr bool kPatterns = true;
+#endif
+    if (kPatterns && patterned) q.base = pattern_color(sc, m.pattern, s, q.over);
     return m;
+}
+
+// The world's lights in order: per-scene builds unroll them with their
+// records as constants (rtc_jit.cpp scene_header); the generic kernels read
+// them wave-uniformly.
+#ifdef RTC_JIT
+template <int I, int E, typename F>
+__device__ inline void jit_light_each(F&& f) {
+    if constexpr (I < E) {
+        f(jit::kLights[I]);
+        jit_light_each<I + 1, E>(f);
+    }
+}
+#endif
+template <typename R, typename F>
+__device__ inline void for_lights(const DevScene<R>& sc, F&& f) {
+#ifdef RTC_JIT
+    if constexpr (sizeof(R) == 4) {
+        jit_light_each<0, jit::kNumLights>(f);
+        return;
+    }
+#endif
+    for (int li = 0; li < sc.n_lights; ++li) f(ld_uniform(&sc.lights[li]));
 }
 
 // calculate_lighting (material.rs:83-114) of one light: ambient always;
@@ -960,8 +988,7 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
     const MaterialRec<R>& m = prepare_hit(sc, o, d, h, q, out.patterned);
     const V3<R> p = q.p, n = q.n, eye = q.eye, over = q.over, base = q.base;
     V3<R> surface = {(R)0, (R)0, (R)0};
-    for (int li = 0; li < sc.n_lights; ++li) {
-        const LightRec<R> L = ld_uniform(&sc.lights[li]);
+    for_lights(sc, [&](const LightRec<R>& L) {
         const V3<R> lpos = {L.position[0], L.position[1], L.position[2]};
         const V3<R> to_light = vsub(lpos, over);
         const R dist = magnitude(to_light);
@@ -976,7 +1003,7 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
         if (!(ldn < (R)0)) shadowed = any_hit(sc, over, ld, dist);
         const V3<R> c = lighting_term(L, m, base, n, eye, ld, ldn, shadowed);
         surface = {surface.x + c.x, surface.y + c.y, surface.z + c.z};
-    }
+    });
     out.surface = surface;
     out.refl_child = out.refr_child = false;
     // shade_hit evaluates Schlick whenever the material is both (world.rs:59-60)
@@ -1243,7 +1270,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
     extern __shared__ __align__(16) unsigned char smem[];
     (void)scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem, true);
-    if (P.stamps && threadIdx.x == 0) P.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#ifdef RTC_JIT
+    // per-scene builds run no diagnostics (RT_FLAG_STAMPS / NO_SHADE / NO_TRACE
+    // launches take the generic kernel, rtc_host.cpp launch)
+    constexpr bool kDiag = false;
+#else
+    const bool kDiag = true;
+#endif
+    if (kDiag && P.stamps && threadIdx.x == 0) P.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     Counts k = {};
     const uint32_t tid = threadIdx.x;
     // Tiles b, b+G, b+2G, ...: with G = n_tiles (kSchedGrid) one tile per
@@ -1266,7 +1300,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         Shaded<R> sh;
         bool hit = false;
         if (valid) {
-            if (P.flags & (RT_FLAG_NO_SHADE | RT_FLAG_NO_TRACE)) {
+            if (kDiag && (P.flags & (RT_FLAG_NO_SHADE | RT_FLAG_NO_TRACE))) {
                 if (P.flags & RT_FLAG_NO_TRACE) {
                     c = d;
                 } else {
@@ -1282,7 +1316,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         if (valid) store_pixel(P, out_idx, c);
     }
     if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
-    if (P.stamps) {
+    if (kDiag && P.stamps) {
         __syncthreads();
         if (threadIdx.x == 0) P.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
     }
@@ -1422,7 +1456,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
     extern __shared__ __align__(16) unsigned char smem_all[];
     const DevScene<R> sc = scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem_all, true);
-    if (P.stamps && threadIdx.x == 0) P.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    // (per-scene pool builds keep the diagnostics: same-box A/B without them
+    // reflect_refract, refraction, metal within 1 %)
+    constexpr bool kDiag = true;
+    if (kDiag && P.stamps && threadIdx.x == 0) P.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     unsigned char* smem = smem_all + (kLds ? P.world_lds : 0);
     __shared__ unsigned int s_tile[2];
     __shared__ int s_top[2];
@@ -1525,7 +1562,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
             if (split) atomicMax(&P.tile_cost[t], c << split);
             else P.tile_cost[t] = c;
         }
-        if (tid == 0 && P.item_log) {  // diagnostics (RT_FLAG_STAMPS): the item's span
+        if (kDiag && tid == 0 && P.item_log) {  // diagnostics (RT_FLAG_STAMPS): the item's span
             const unsigned long long k = atomicAdd(&P.item_log[0], 1ull);
             P.item_log[1 + 3 * k] = item | (unsigned long long)blockIdx.x << 32;
             P.item_log[2 + 3 * k] = tile_start;
@@ -1533,7 +1570,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         }
     }
     if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
-    if (P.stamps) {
+    if (kDiag && P.stamps) {
         __syncthreads();
         if (threadIdx.x == 0) P.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
     }
