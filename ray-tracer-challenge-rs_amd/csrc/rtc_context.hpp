@@ -163,6 +163,8 @@ struct rt_context {
     std::vector<rtc::ShapeRec<float>> jit_shapes;
     std::vector<rtc::LightRec<float>> jit_lights;  // per-scene builds unroll the lights as constants
     bool jit_patterns = true;                      // some material has a pattern (else pattern code is dropped)
+    uint32_t jit_pattern_kinds = ~0u;              // pattern kinds in the world's table (bit per RT_PATTERN_*)
+    bool jit_transparent = true;                   // some material is transparent (else no refraction code)
     int32_t jit_begin[rtc::kNumKinds + 1] = {};
     hipFunction_t jit_fn[4] = {};
     std::shared_ptr<rtc::CodeBuild> jit_build[4];  // the build each variant waits for (host thread)

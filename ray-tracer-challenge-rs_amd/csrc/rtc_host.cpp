@@ -934,6 +934,14 @@ int capture_jit_table(rt_context* ctx) {
     std::vector<MaterialRec<float>> mats(nm);
     if (nm) RT_HIP(hipMemcpy(mats.data(), ctx->w32.materials, nm * sizeof(MaterialRec<float>), hipMemcpyDeviceToHost));
     ctx->jit_patterns = std::any_of(mats.begin(), mats.end(), [](const MaterialRec<float>& m) { return m.pattern >= 0; });
+    ctx->jit_transparent =
+        std::any_of(mats.begin(), mats.end(), [](const MaterialRec<float>& m) { return m.transparency != 0.0f; });
+    const int32_t np = ctx->w32.scene.n_patterns;
+    std::vector<PatternRec<float>> pats(np);
+    if (np) RT_HIP(hipMemcpy(pats.data(), ctx->w32.patterns, np * sizeof(PatternRec<float>), hipMemcpyDeviceToHost));
+    ctx->jit_pattern_kinds = 0;
+    for (const PatternRec<float>& q : pats)  // every kind a pattern_color walk can meet (complex sub-patterns included)
+        ctx->jit_pattern_kinds |= 1u << std::min<uint32_t>((uint32_t)q.kind, RT_PATTERN_TEST);
     for (int v = 0; v < 4; ++v) {
         ctx->jit_fn[v] = nullptr;
         ctx->jit_build[v].reset();

@@ -816,6 +816,14 @@ __device__ inline V3<R> hit_normal(const ShapeRec<R>& s, int slot, int kind, V3<
 }
 
 // Pattern::color_at_shape (pattern.rs:10-14) and the five color_at bodies.
+// A per-scene build compiles in only the kinds its world's table holds
+// (jit::kPatternKinds: the walk can meet no other).
+#ifdef RTC_JIT
+#define RTC_PATTERN_KIND(k) \
+    if (!((jit::kPatternKinds >> (k)) & 1u)) __builtin_unreachable()
+#else
+#define RTC_PATTERN_KIND(k) (void)0
+#endif
 template <typename R>
 __device__ inline V3<R> pattern_color(const DevScene<R>& sc, int pid, const ShapeRec<R>& s, V3<R> p) {
     using T = Real<R>;
@@ -824,9 +832,11 @@ __device__ inline V3<R> pattern_color(const DevScene<R>& sc, int pid, const Shap
     for (int guard = 0; guard < 16; ++guard) {
         switch (pr->kind) {
             case RT_PATTERN_STRIPE:  // stripe_pattern.rs:24-31
+                RTC_PATTERN_KIND(RT_PATTERN_STRIPE);
                 return odd_i64(T::floor(pp.x)) ? v3(pr->color_b[0], pr->color_b[1], pr->color_b[2])
                                                 : v3(pr->color_a[0], pr->color_a[1], pr->color_a[2]);
             case RT_PATTERN_GRADIENT: {  // gradient_pattern.rs:24-31 (ping-pong)
+                RTC_PATTERN_KIND(RT_PATTERN_GRADIENT);
                 R f = T::fabs(pp.x - T::trunc(pp.x));
                 if (odd_i64(pp.x)) f = (R)1 - f;
                 return {pr->color_a[0] + (pr->color_b[0] - pr->color_a[0]) * f,
@@ -834,19 +844,23 @@ __device__ inline V3<R> pattern_color(const DevScene<R>& sc, int pid, const Shap
                         pr->color_a[2] + (pr->color_b[2] - pr->color_a[2]) * f};
             }
             case RT_PATTERN_RING: {  // ring_pattern.rs:25-32
+                RTC_PATTERN_KIND(RT_PATTERN_RING);
                 const R r = T::floor(T::sqrt(pp.x * pp.x + pp.z * pp.z));
                 return odd_i64(r) ? v3(pr->color_b[0], pr->color_b[1], pr->color_b[2])
                                   : v3(pr->color_a[0], pr->color_a[1], pr->color_a[2]);
             }
             case RT_PATTERN_CHECKER: {  // checker_pattern.rs:24-31
+                RTC_PATTERN_KIND(RT_PATTERN_CHECKER);
                 const R sum = T::floor(pp.x) + T::floor(pp.y) + T::floor(pp.z);
                 return odd_i64(sum) ? v3(pr->color_b[0], pr->color_b[1], pr->color_b[2])
                                     : v3(pr->color_a[0], pr->color_a[1], pr->color_a[2]);
             }
             case RT_PATTERN_COMPLEX:  // complex_pattern.rs:25-32: sub transforms ignored
+                RTC_PATTERN_KIND(RT_PATTERN_COMPLEX);
                 pr = &sc.lpats[odd_i64(T::floor(pp.x)) ? pr->sub_b : pr->sub_a];
                 continue;
             default:  // TestPattern (pattern.rs:55-58)
+                RTC_PATTERN_KIND(RT_PATTERN_TEST);
                 return pp;
         }
     }
@@ -1009,9 +1023,14 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
     // shade_hit evaluates Schlick whenever the material is both (world.rs:59-60)
     out.schlick = (m.reflectiveness > (R)0) & (m.transparency > (R)0);
     if constexpr (kChildren) {
-        const bool reflective = m.reflectiveness > (R)0, transparent = m.transparency > (R)0;
+#ifdef RTC_JIT
+        constexpr bool kTransparent = jit::kTransparent;  // per-scene build: no glass, no refraction code
+#else
+        constexpr bool kTransparent = true;
+#endif
+        const bool reflective = m.reflectiveness > (R)0, transparent = kTransparent && m.transparency > (R)0;
         R n1 = (R)1, n2 = (R)1;
-        if (m.transparency != (R)0) refractive_indices<R, kDup>(sc, o, d, h, n1, n2);
+        if (kTransparent && m.transparency != (R)0) refractive_indices<R, kDup>(sc, o, d, h, n1, n2);
         // Schlick mixing only when both (world.rs:59-66)
         R fr = (R)1, ft = (R)1;
         if (reflective && transparent) {  // computed_hit.rs:50-68
@@ -1037,7 +1056,7 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
             out.refl_child = true;
             push(over, reflect(d, n), m.reflectiveness * fr);
         }
-        if (remaining > 0 && m.transparency != (R)0) {  // world.rs:130-157
+        if (kTransparent && remaining > 0 && m.transparency != (R)0) {  // world.rs:130-157
             out.refr_eval = true;
             const R nr = T::div(n1, n2);
             const R cos_i = dot(eye, n);
