@@ -69,13 +69,32 @@ def test_per_scene_kernel_is_bit_identical(gpu_ctx, rtc, name, depth):
     assert _counts(sa) == _counts(sb)
 
 
-def test_per_scene_kernel_all_kinds(gpu_ctx):
+@pytest.mark.parametrize("depth", [0, 6])
+def test_per_scene_kernel_all_kinds(gpu_ctx, depth):
+    """Every shape and pattern kind (a complex pattern's sub-patterns
+    included: the per-scene build compiles only the kinds its world holds),
+    glass, two lights: the per-scene frame equals the generic one."""
     from test_gpu_parity import _all_shapes_world
     from rtc_amd import world as W
     cam = W.camera(160, 120, 1.0, (0, 3, -8), (0, 0.8, 0), (0, 1, 0))
-    a, sa, b, sb, _ = _both(gpu_ctx, _all_shapes_world(), cam, 0)
+    a, sa, b, sb, _ = _both(gpu_ctx, _all_shapes_world(), cam, depth)
     if b is not None:
         assert np.array_equal(a, b) and _counts(sa) == _counts(sb)
+
+
+def test_per_scene_kernel_complex_pattern_only(gpu_ctx):
+    """A world whose only material pattern is a complex one: its stripe and
+    checker sub-patterns must be compiled into the per-scene build."""
+    from rtc_amd import world as W
+    pat = W.complex_pattern(W.stripe_pattern((1, 1, 1), (0, 0, 0)), W.checker_pattern((1, 0, 0), (0, 1, 0)))
+    shapes = [W.plane(W.Material(reflectiveness=0.4)),
+              W.sphere(W.Material(pattern=pat), W.mat_mul(W.translation(0, 1, 0), W.scaling(1.5, 1.5, 1.5)))]
+    tables = W.World([W.Light((-10, 10, -10))], shapes).tables()
+    cam = W.camera(160, 120, 1.0, (0, 2, -6), (0, 1, 0), (0, 1, 0))
+    for depth in (0, 6):
+        a, sa, b, sb, _ = _both(gpu_ctx, tables, cam, depth)
+        if b is not None:
+            assert np.array_equal(a, b) and _counts(sa) == _counts(sb)
 
 
 def _fresh_world(rtc, name, salt):
