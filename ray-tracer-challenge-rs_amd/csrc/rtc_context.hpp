@@ -110,8 +110,6 @@ struct rt_context {
     bool cold_center = true;
     uint32_t* d_cold_order = nullptr;  // centre-out order + item count, for cold_w x cold_h
     uint32_t cold_w = 0, cold_h = 0;
-    double cold_prio = 0;          // RTC_COLD_PRIO: the first cold_prio x grid centre-out tiles at priority 2
-    uint32_t cold_prio_n = 0;      // ... as built into d_cold_order
     // Tiles costing more than split_factor x the mean workgroup load are
     // handed out in parts (order_tiles); RTC_SPLIT=0 never splits.  Round-3
     // sweep (per-scene kernels, slowest of 8 shards at 4K / 1-GPU frame):

@@ -487,8 +487,7 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
         // No costs yet: tiles nearest the image centre first.  The order
         // depends on the canvas only, so it is built and uploaded once per
         // canvas size into its own buffer (order_tiles reuses d_tile_order).
-        const uint32_t cold_prio_n = (uint32_t)std::min(4e9, ctx->cold_prio * grid);
-        if (!ctx->d_cold_order || ctx->cold_w != P.width || ctx->cold_h != P.height || ctx->cold_prio_n != cold_prio_n) {
+        if (!ctx->d_cold_order || ctx->cold_w != P.width || ctx->cold_h != P.height) {
             const uint32_t n = P.n_tiles, tx = P.tiles_x;
             std::vector<std::pair<uint64_t, uint32_t>> key(n);
             const int64_t cx = (int64_t)P.width, cy = (int64_t)P.height;  // doubled centre
@@ -499,8 +498,7 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
             }
             std::sort(key.begin(), key.end());
             std::vector<uint32_t> v(n + 1);
-            // RTC_COLD_PRIO: the first cold_prio x grid tiles (nearest the centre) at priority 2
-            for (uint32_t i = 0; i < n; ++i) v[i] = key[i].second | (i < cold_prio_n ? 2u << kItemPrioShift : 0u);
+            for (uint32_t i = 0; i < n; ++i) v[i] = key[i].second;
             v[n] = n;
             (void)hipFree(ctx->d_cold_order);
             ctx->d_cold_order = nullptr;
@@ -508,7 +506,6 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
             RT_HIP(hipMemcpy(ctx->d_cold_order, v.data(), v.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
             ctx->cold_w = P.width;
             ctx->cold_h = P.height;
-            ctx->cold_prio_n = cold_prio_n;
         }
         P.tile_order = ctx->d_cold_order;
         P.item_count = ctx->d_cold_order + P.n_tiles;
@@ -837,7 +834,6 @@ int create_device_context(int device_ordinal, rt_context** out) {
         if (n >= 3) ctx->probe_split = sp != 0;
     }
     if (const char* e = std::getenv("RTC_URGENT_GRADED")) ctx->urgent_graded = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("RTC_COLD_PRIO")) ctx->cold_prio = std::atof(e);
     if (const char* e = std::getenv("RTC_ORDER_BUILDS")) ctx->order_max_builds = std::atoi(e);
     if (const char* e = std::getenv("RTC_DIRECT_GRID")) ctx->direct_grid = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("RTC_JIT"))
