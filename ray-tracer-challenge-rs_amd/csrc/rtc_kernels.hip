@@ -470,8 +470,8 @@ __device__ inline void for_all_kinds(const DevScene<R>& sc, F&& f) {
 // same.  The ray meets the ball iff its line passes within r of the center,
 // |d x oc|^2 <= r^2 |d|^2, and the center is not behind an outside origin
 // (oc.d < 0 with |oc| > r makes |o + t d - C|^2 > r^2 for every t >= 0).
-// Not used by the refractive-index walk (it counts t < 0 entries; a
-// line-only variant measured slower there: its transparent shapes are large).
+// The refractive-index walk counts t < 0 entries too and takes the line-only
+// test below (wave_line_may_hit, per-scene builds).
 // Wave-wide OR of a lane predicate (active lanes).  The raw builtin: HIP's
 // __ballot(int) turns the predicate into a VGPR and compares it again.
 __device__ inline bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
@@ -503,6 +503,27 @@ __device__ inline bool wave_may_hit(const ShapeRec<R>& s, V3<R> o, V3<R> d, R dd
     // the compiler materialise it in a VGPR and compare it again: 2 VALU)
     const unsigned long long front = __builtin_amdgcn_ballot_w64(tc >= (R)0) | __builtin_amdgcn_ballot_w64(oo <= r2);
     return (front & __builtin_amdgcn_ballot_w64(Real<R>::madd(oo, kKeep, -r2) * dd <= tc * tc)) != 0;
+}
+
+// The refractive-index walk's cull: entries at every t count there (t < 0
+// included), so only the line test applies: no active lane's line passes
+// within the bound's radius (|d x oc|^2 > r^2 |d|^2, with wave_may_hit's
+// conservative margin) means no lane has an entry of this shape.  Per-scene
+// builds only (constant bounds, kWalkCull); the generic kernel measured slower
+// with it (round 2: its loads of the bound cost more than the scans it saved).
+#ifndef RTC_WALK_CULL_MIN
+#define RTC_WALK_CULL_MIN 4
+#endif
+template <typename R, int K>
+__device__ inline bool wave_line_may_hit(const ShapeRec<R>& s, V3<R> o, V3<R> d, R dd) {
+    if constexpr (K == RT_SHAPE_PLANE) return true;
+    const R r2 = s.bound[3];
+    if constexpr (K != RT_SHAPE_SPHERE && K != RT_SHAPE_CUBE)
+        if (!(r2 >= (R)0)) return true;
+    const V3<R> oc = {s.bound[0] - o.x, s.bound[1] - o.y, s.bound[2] - o.z};
+    constexpr R kKeep = sizeof(R) == 4 ? (R)(1 - 1e-5) : (R)(1 - 1e-12);
+    const R tc = dot(oc, d), oo = dot(oc, oc);
+    return wave_any(Real<R>::madd(oo, kKeep, -r2) * dd <= tc * tc);
 }
 
 // Per-scene build only: the ray's registers pass through an empty asm at the
@@ -619,6 +640,9 @@ struct Blocker {
 // is_in_shadow (world.rs:98-112): any casting shape with 0 <= t < distance.
 template <typename R>
 __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) {
+#ifdef RTC_ABLATE_SHADOW  // diagnostic builds only (scripts/gpu_r3ai.sh): time without shadow rays
+    return false;
+#endif
     Blocker<R> b;
     const R dd = dot(d, d);
     for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
@@ -649,6 +673,11 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) 
 template <typename R, bool kDup>
 __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> d, const Hit<R>& h, R& n1,
                                           R& n2) {
+#ifdef RTC_ABLATE_WALK  // diagnostic builds only (scripts/gpu_r3ai.sh): time without the walk
+    n1 = (R)1;
+    n2 = sc.lmats[sc.lshapes[h.slot].material].refractive_index;
+    return;
+#endif
     struct Key {
         R t;
         int w, e;
@@ -699,18 +728,30 @@ __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> 
             e += v ? 1 : 0;
         });
     };
+#if defined(RTC_JIT) && !defined(RTC_NO_WALK_CULL)
+    // worlds of a few bounded shapes (refraction.yaml: a lens of two spheres
+    // over a plane) have nothing to cull: every line meets the lens's bounds,
+    // and the tests cost 2.4 % there; from RTC_WALK_CULL_MIN bounded shapes on
+    // they pay (cover 1080p -16 %, reflect_refract -2 %)
+    constexpr int kBounded = jit::kBegin[kNumKinds] - (jit::kBegin[RT_SHAPE_PLANE + 1] - jit::kBegin[RT_SHAPE_PLANE]);
+    constexpr bool kWalkCull = sizeof(R) == 4 && kBounded >= RTC_WALK_CULL_MIN;
+#else
+    constexpr bool kWalkCull = false;
+#endif
+    const R dd = dot(d, d);
     if constexpr (kDup) {
         const uint32_t hit_class = (uint32_t)sc.lshapes[h.slot].flags >> kShapeClassShift;
         int count = 0;  // over the current class's records
         Key last{};
         for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
-            scan.template operator()<K>(s, count, last);
+            if (!kWalkCull || wave_line_may_hit<R, K>(s, o, d, dd)) scan.template operator()<K>(s, count, last);
             if (!(s.flags & kShapeClassEnd)) return;  // wave-uniform: more members follow
             settle(count, last, s, (uint32_t)s.flags >> kShapeClassShift == hit_class);
             count = 0;
         });
     } else {
         for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
+            if (kWalkCull && !wave_line_may_hit<R, K>(s, o, d, dd)) return;  // no entries: nothing to settle
             int count = 0;
             Key last{};
             scan.template operator()<K>(s, count, last);
