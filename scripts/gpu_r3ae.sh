@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: RTC_SPLIT_STICKY was measured, rejected and removed from the tree)
 # Sticky splits (RTC_SPLIT_STICKY) and order-build count on shards and whole frames
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

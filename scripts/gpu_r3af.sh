@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: RTC_COLD_PRIO was measured, rejected and removed from the tree)
 # Cold launches: the first centre-out tiles at priority 2 (RTC_COLD_PRIO = fraction of the grid); new JIT tests
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

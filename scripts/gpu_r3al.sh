@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: RTC_POOL_GRID was measured, rejected and removed from the tree)
 # Pool kernel grid below the resident one (RTC_POOL_GRID) on 8-way shards and whole frames
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: RTC_OVERLAP was measured, rejected and removed from the tree)
 # (1) overlapped-items pool kernel (RTC_OVERLAP build _lib_ov): smoke frame, parity/exactness tests, A/B
 # (2) cold-launch probe sweep; (3) direct-kernel PMC ablation
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: RTC_AGE_PRIO was measured, rejected and removed from the tree)
 # Age-based wave priority (RTC_AGE_PRIO=g1,g2,g3): warm and cold kernel ms, 2 rounds; 8-shard cover/table
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: RTC_PRIO_CAP was measured, rejected and removed from the tree)
 # Priority cap by queue position (RTC_PRIO_CAP=f3,f2,f1): shards and whole frames
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

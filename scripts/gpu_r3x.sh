@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: RTC_PRIO_CAP and RTC_OVERLAP was measured, rejected and removed from the tree)
 # (1) priority cap by queue position (RTC_PRIO_CAP) on shards; (2) overlapped-items pool kernel (_lib_ov): tests, shards, frames
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
