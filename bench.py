@@ -74,6 +74,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--flags", type=int, default=0, help="RT_FLAG_* diagnostic ablations (profiling only)")
+    ap.add_argument("--one-shot-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -187,8 +188,58 @@ def resolve(args, tiled):
     return a
 
 
+def one_shot_child(args):
+    """A drop-in one-shot render in a fresh, torch-free process (what the
+    reference's only caller does, main.rs:13-22: load, then time one
+    render call; a Rust host would bind librtc the same way): context
+    creation (the HIP runtime starts here), scene upload, then one
+    synchronous rt_render into a host canvas (the cold generic kernel, module
+    load and PCIe copy included).  Prints one JSON object."""
+    os.environ["RTC_NO_TORCH"] = "1"
+    import numpy as np
+    import rtc_amd
+    from rtc_amd import scene_io
+    a = resolve(args, False)
+    scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{a.scene}.json"))
+    cam = rtc_amd.camera_resize(scene.camera, a.width, a.height)
+    canvas = np.zeros((cam.height, cam.width, 3), dtype=np.float32 if a.precision == "f32" else np.float64)
+    t0 = time.perf_counter()
+    ctx = rtc_amd.Context(0)
+    t1 = time.perf_counter()
+    ctx.upload(scene)
+    t2 = time.perf_counter()
+    _, st = ctx.render(cam, a.depth, a.precision, "real", out=canvas)
+    t3 = time.perf_counter()
+    ctx.set_jit(rtc_amd.RT_JIT_OFF)  # (no per-scene build from a one-shot process)
+    _, st2 = ctx.render(cam, a.depth, a.precision, "real", out=canvas)  # the same call, warm
+    t4 = time.perf_counter()
+    print(json.dumps({"context_ms": (t1 - t0) * 1e3, "upload_ms": (t2 - t1) * 1e3, "render_ms": (t3 - t2) * 1e3,
+                      "total_ms": (t3 - t0) * 1e3, "render_kernel_ms": st["kernel_ms"],
+                      "second_render_ms": (t4 - t3) * 1e3, "jit_used": ctx.jit_status()["used"],
+                      "workload": f"{a.scene}@{cam.width}x{cam.height},depth={a.depth},{a.precision}"}))
+    ctx.close()
+
+
+def one_shot(args):
+    """Run one_shot_child in a subprocess (rank 0, N = 1); None if it fails."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--one-shot-child", "--precision", args.precision]
+    for k in ("scene", "width", "height", "depth"):
+        if getattr(args, k) is not None:
+            cmd += [f"--{k}", str(getattr(args, k))]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        return json.loads(lines[-1]) if r.returncode == 0 and lines else {"error": (r.stderr or r.stdout)[-400:]}
+    except Exception as e:  # noqa: BLE001  (a diagnostic: never fails the bench line)
+        return {"error": repr(e)[:400]}
+
+
 def main():
     args = parse()
+    if args.one_shot_child:
+        one_shot_child(args)
+        return
     import torch
     import torch.distributed as dist
 
@@ -246,6 +297,7 @@ def measure(args, tiled, world, rank, local):
     # Only rank 0 holds the world, as the reference's single caller does
     t_first = time.perf_counter()
     scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{args.scene}.json")) if rank == 0 else None
+    phase = {"scene_load_ms": (time.perf_counter() - t_first) * 1e3}
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
     rdtype = torch.uint8 if args.out == "u8" else (torch.float32 if args.precision == "f32" else torch.float64)
@@ -253,8 +305,12 @@ def measure(args, tiled, world, rank, local):
         # the library's multi-GPU context: RCCL communicator from a unique id,
         # scene broadcast inside rt_scene_upload, strips gathered onto rank 0
         uid = rdist.share_unique_id(rank) if world > 1 else rtc_amd.comm_unique_id()
+        t = time.perf_counter()
         ctx = rtc_amd.Context.rank(local, world, rank, uid)
+        phase["context_ms"] = (time.perf_counter() - t) * 1e3
+        t = time.perf_counter()
         ctx.upload(scene if rank == 0 else None)
+        phase["upload_ms"] = (time.perf_counter() - t) * 1e3
         cam0 = rtc_amd.camera_resize(scene.camera, args.width, args.height) if rank == 0 else None
         cam = rdist.share_camera(cam0, rank) if world > 1 else cam0
         image = torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda") if rank == 0 else None
@@ -263,17 +319,27 @@ def measure(args, tiled, world, rank, local):
         if world > 1:
             scene = rdist.broadcast_scene(scene, rank, "cpu")
         cam = rtc_amd.camera_resize(scene.camera, args.width, args.height)
+        t = time.perf_counter()
         ctx = rtc_amd.Context(local)
+        phase["context_ms"] = (time.perf_counter() - t) * 1e3
+        t = time.perf_counter()
         ctx.upload(scene)
+        phase["upload_ms"] = (time.perf_counter() - t) * 1e3
         image = torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda")
         out_ptr = image.data_ptr()
 
     def step():
         ctx.render_device(cam, out_ptr, sptr, args.depth, args.precision, args.out, (0, 1), args.flags)
 
+    t = time.perf_counter()
     step()  # first frame: scene transfer, context, upload and one render
     torch.cuda.synchronize()
+    phase["first_render_ms"] = (time.perf_counter() - t) * 1e3
     first_frame_ms = (time.perf_counter() - t_first) * 1e3
+    if rank == 0:  # the frame into host memory (the rest of a one-shot Camera::render)
+        t = time.perf_counter()
+        image.cpu()
+        phase["d2h_ms"] = (time.perf_counter() - t) * 1e3
     # The per-scene kernel (rtc.h RT_JIT_AUTO): the second large frame starts
     # its hipRTC build on a host thread and renders with the generic kernel;
     # frames switch once it lands.  The bench lets it land before the warm-up
@@ -325,6 +391,8 @@ def measure(args, tiled, world, rank, local):
 
     rays = after["rays"] - before["rays"]
     flops = after["algorithmic_flops"] - before["algorithmic_flops"]
+    # rays per frame by kind (SURVEY.md §8d semantics; this process's GPU)
+    by_kind = {k: (after[k] - before[k]) // args.steps for k in ("primary", "shadow", "reflect", "refract")}
     elapsed, total_rays = rdist.job_totals(elapsed, rays, "cpu")
     extra = {}
     if tiled:
@@ -402,7 +470,9 @@ def measure(args, tiled, world, rank, local):
         if tiled:
             line["roofline"]["kernel"] = "rank 0's shard launch (median of 5 instrumented frames)"
         line.update(extra)
+        line["rays_by_kind"] = by_kind
         line["first_frame_ms"] = first_frame_ms
+        line["first_frame_breakdown"] = phase
         try:  # per-scene build (hipRTC, or a load from RTC_JIT_CACHE) on its host thread, after the first frame
             js = ctx.jit_status()
             line["jit_build_ms"] = js["compile_ms"]
@@ -414,7 +484,7 @@ def measure(args, tiled, world, rank, local):
         if not tiled and world == 1:
             if ctx.scene.has_secondary() and args.depth > 0:
                 # cold launch: the first frame after an upload has no recorded
-                # tile costs; its order comes from the cost probe
+                # tile costs; its tiles are handed out centre-out
                 cold = []
                 for _ in range(3):
                     ctx.upload(scene)
@@ -431,6 +501,28 @@ def measure(args, tiled, world, rank, local):
                 ctx.render(cam, args.depth, args.precision, args.out, out=canvas)
                 lat.append((time.perf_counter() - t) * 1e3)
             line["host_frame_ms"] = float(np.median(lat))
+            # the PCIe floor of that copy: the frame's bytes at the measured
+            # pinned device-to-host rate of this box's link
+            pinned = torch.empty(image.shape, dtype=image.dtype, pin_memory=True)
+            pinned.copy_(image, non_blocking=True)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(5):
+                pinned.copy_(image, non_blocking=True)
+            torch.cuda.synchronize()
+            d2h_s = (time.perf_counter() - t) / 5
+            line["host_frame_floor_ms"] = d2h_s * 1e3
+            line["d2h_gbs"] = image.numel() * image.element_size() / d2h_s / 1e9
+            # rays per generation (each bounce's wavefront size):
+            # one untimed diagnostic frame of the generic kernel (RT_FLAG_GENERATIONS)
+            _, _, gen = ctx.render_generations(cam, args.depth, args.precision)
+            light_n = len(scene.lights)
+            line["rays_by_generation"] = {"traced": gen["traced"], "shaded": gen["shaded"],
+                                          "shadow": [light_n * v for v in gen["shaded"]],
+                                          "note": "generation g = bounce g (0 = camera rays); traced = radiance "
+                                                  "rays (the wavefront), shadow = L per shaded hit"}
+        if world == 1 and not tiled:
+            line["one_shot"] = one_shot(args)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(scene, cam, args.depth, args.cpu_seconds)
             line["cpu_baseline"]["configs0_serial"] = cpu_serial_configs0(min(3.0, args.cpu_seconds / 4))

@@ -166,6 +166,9 @@ typedef struct rt_camera_desc {
 #define RT_FLAG_STAMPS 8u      /* record per-workgroup start/end timestamps */
 #define RT_FLAG_FAIL_LAUNCH 16u /* fail with RT_ERR_HIP after planning, before
                                   * the enqueue (tests the error path)      */
+#define RT_FLAG_GENERATIONS 32u /* also count rays per generation (generic
+                                  * kernels; rt_read_generation_counts).
+                                  * Pixels and rt_stats are unchanged.      */
 
 typedef struct rt_render_options {
     uint32_t max_depth;    /* `remaining` of the primary ray; 6 = reference */
@@ -322,8 +325,12 @@ int rt_debug_normal(rt_context* ctx, uint32_t shape, const double* points, uint6
  * last build error (a failed build keeps the generic kernel for that world).
  * rt_jit_wait: block until this context's builds in flight have finished
  * (at most timeout_ms; < 0 = no limit); *pending = builds still running.
- * A context destroyed with a build in flight does not wait for it; librtc
- * joins its build threads when it is unloaded.  Builds are also cached on
+ * A context destroyed with a build in flight does not wait for it: the
+ * compile runs in a child process (rtc_jitc) and a DETACHED thread of this
+ * process waits for it, runs librtc code when it ends, and is never joined.
+ * So librtc must not be unloaded (dlclose) while rt_jit_wait reports pending
+ * builds; process exit is safe (the orphaned compiler still finishes and
+ * fills the disk cache).  Builds are also cached on
  * disk across processes: env RTC_JIT_CACHE = a directory, or 0 for none
  * (default $XDG_CACHE_HOME/rtc_jit, else ~/.cache/rtc_jit). */
 enum { RT_JIT_OFF = 0, RT_JIT_SYNC = 1, RT_JIT_AUTO = 2, RT_JIT_EAGER = 3 };
@@ -333,6 +340,20 @@ int rt_jit_wait(rt_context* ctx, double timeout_ms, int* pending);
 
 /* Cumulative device counters since context creation (after a sync). */
 int rt_read_counters(rt_context* ctx, rt_stats* totals);
+
+/* Rays per generation (the wavefront's size at each bounce), cumulative
+ * over this context's launches made with RT_FLAG_GENERATIONS.  Indexed by
+ * `remaining` (world.rs:70-86): a primary ray is traced at max_depth and a
+ * reflected or refracted child at its parent's remaining - 1
+ * (world.rs:114-157), so generation g of a frame rendered at depth D is
+ * entry D - g.  traced = radiance rays traced (internal_color_at calls),
+ * shaded = hits shaded; each shaded hit casts one shadow ray per light
+ * (world.rs:46-52).  Group contexts report the calling process's GPUs. */
+typedef struct rt_generation_counts {
+    uint64_t traced[RT_MAX_SUPPORTED_DEPTH + 1];
+    uint64_t shaded[RT_MAX_SUPPORTED_DEPTH + 1];
+} rt_generation_counts;
+int rt_read_generation_counts(rt_context* ctx, rt_generation_counts* out);
 
 /* De-interleave gathered shard strips (shard-major, each rt_shard_rows tall)
  * into one row-major image on the device, on `hip_stream`. */

@@ -107,6 +107,7 @@ void fill_stats(const Counters& k, rt_stats* s) {
 }
 
 thread_local std::string g_err;
+thread_local Counters g_last;  // counters of this thread's last render / color_at (orc_last_generations)
 
 }  // namespace
 
@@ -153,6 +154,7 @@ int orc_render(const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc*
         Counters k;
         render_rows(camera_from(*cam), w, (int)depth, row_begin, row_end, threads, out, &k);
         fill_stats(k, stats);
+        g_last = k;
         return 0;
     } catch (const std::exception& e) {
         g_err = e.what();
@@ -177,11 +179,22 @@ int orc_color_at(const rt_shape_desc* shapes, uint32_t ns, const rt_material_des
             out[3 * i + 2] = c.b;
         }
         fill_stats(k, stats);
+        g_last = k;
         return 0;
     } catch (const std::exception& e) {
         g_err = e.what();
         return -1;
     }
+}
+
+// Per-generation counts of this thread's last orc_render / orc_color_at,
+// indexed by `remaining` (Counters::traced_at / shaded_at): 17 entries each.
+int orc_last_generations(uint64_t* traced, uint64_t* shaded) {
+    for (int i = 0; i <= Counters::kMaxRemaining; ++i) {
+        traced[i] = g_last.traced_at[i];
+        shaded[i] = g_last.shaded_at[i];
+    }
+    return 0;
 }
 
 }  // extern "C"

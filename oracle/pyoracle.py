@@ -58,6 +58,8 @@ def lib():
         L.orc_inverse.argtypes = [P(C.c_double), P(C.c_double)]
         L.orc_inverse.restype = C.c_int
         L.orc_last_error.restype = C.c_char_p
+        L.orc_last_generations.argtypes = [P(C.c_uint64), P(C.c_uint64)]
+        L.orc_last_generations.restype = C.c_int
         _lib = L
     return _lib
 
@@ -87,6 +89,15 @@ def color_at(scene, rays, depth: int = 6):
     _check(lib().orc_color_at(*scene.args(), rays.ctypes.data_as(C.POINTER(C.c_double)), rays.shape[0], depth,
                               out.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st)))
     return out, st.as_dict()
+
+
+def last_generations():
+    """(traced, shaded) per `remaining` 0..16 of this thread's last render / color_at
+    (a child ray runs at its parent's remaining - 1; the primary at the depth)."""
+    t = np.zeros(17, dtype=np.uint64)
+    s = np.zeros(17, dtype=np.uint64)
+    _check(lib().orc_last_generations(t.ctypes.data_as(C.POINTER(C.c_uint64)), s.ctypes.data_as(C.POINTER(C.c_uint64))))
+    return t, s
 
 
 def camera(width, height, fov, frm, to, up):

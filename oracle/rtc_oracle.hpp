@@ -717,13 +717,22 @@ inline double schlick(const Comps& c) {
 }
 
 // Counters in the reference's ray semantics.
+// Per generation, indexed by `remaining` (world.rs:70-86; a child runs at
+// its parent's remaining - 1): radiance rays traced (internal_color_at
+// calls) and hits shaded.  Depths above kMaxRemaining are not counted.
 struct Counters {
+    static constexpr int kMaxRemaining = 16;  // rtc.h RT_MAX_SUPPORTED_DEPTH
     uint64_t primary = 0, shadow = 0, reflect = 0, refract = 0, shaded = 0;
     uint64_t lit_patterned = 0, refract_evals = 0, schlick_evals = 0;
+    uint64_t traced_at[kMaxRemaining + 1] = {}, shaded_at[kMaxRemaining + 1] = {};
     void merge(const Counters& o) {
         primary += o.primary; shadow += o.shadow; reflect += o.reflect; refract += o.refract;
         shaded += o.shaded; lit_patterned += o.lit_patterned; refract_evals += o.refract_evals;
         schlick_evals += o.schlick_evals;
+        for (int i = 0; i <= kMaxRemaining; ++i) {
+            traced_at[i] += o.traced_at[i];
+            shaded_at[i] += o.shaded_at[i];
+        }
     }
 };
 
@@ -779,11 +788,14 @@ struct World {
     }
     // world.rs:70-86
     Color internal_color_at(const Ray& r, Hits& xs, int remaining, Counters* k = nullptr) const {
+        const bool counted = k && remaining >= 0 && remaining <= Counters::kMaxRemaining;
+        if (counted) k->traced_at[remaining]++;
         collect_intersections(r, xs);
         Hits shading;
         const Hit* h = hit(xs);
         if (!h) return BLACK;
         if (k) k->shaded++;
+        if (counted) k->shaded_at[remaining]++;
         Comps c = prepare_computations(*h, r, xs);
         return shade_hit(c, shading, remaining, k);
     }

@@ -129,7 +129,7 @@ bool ends_with(const std::string& s, const char* suffix) {
 
 extern "C" int rt_image_write_format(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height,
                                      int format) {
-    if (!path || !*path || (!rgb && (size_t)width * height) || format < RT_IMAGE_AUTO ||
+    if (!path || !*path || (!rgb && (size_t)width * height != 0) || format < RT_IMAGE_AUTO ||
         format > RT_IMAGE_PPM_BINARY)
         return rtc::set_error(RT_ERR_INVALID, "rt_image_write: bad arguments");
     if (format == RT_IMAGE_AUTO) format = ends_with(path, ".png") ? RT_IMAGE_PNG : RT_IMAGE_PPM;

@@ -76,6 +76,7 @@ struct rt_context {
     unsigned long long* d_tile_counter = nullptr;  // two sets of queue heads (launch: dynamic schedule)
     int head_set = 0;                              // the set the next dynamic launch uses
     unsigned long long* d_counters = nullptr;  // kNumCounters cumulative
+    unsigned long long* d_gen_counts = nullptr;  // RT_FLAG_GENERATIONS: traced, shaded x kGenSlots, cumulative
     int32_t* d_error = nullptr;
     bool have_scene = false;
     rtc::DeviceWorld<float> w32;

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -558,6 +559,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     P.tile_counter = ctx->d_tile_counter;
     P.counters = ctx->d_counters;
     P.error_flag = ctx->d_error;
+    if (flags & RT_FLAG_GENERATIONS) P.gen_counts = ctx->d_gen_counts;
     if (P.n_tiles == 0) return RT_OK;
     if ((rc = order_after_last(ctx, stream))) return rc;
     LaunchShape ls;
@@ -576,6 +578,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
             ctx->spill_bytes = need;
         }
         P.spill = ctx->d_spill;
+        P.spill_blocks = (uint32_t)(ctx->spill_bytes / ((size_t)8 * (ls.cap - ls.lcap) * sizeof(R)));
     }
     P.persistent = ls.sched;
     P.flags = flags;
@@ -637,7 +640,8 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     // large f32 frames run the per-scene build of the same kernel (rtc_jit.cpp)
     hipFunction_t jf = nullptr;
     if constexpr (sizeof(R) == 4) {
-        const bool want = cam && !dup && !(flags & (RT_FLAG_STAMPS | RT_FLAG_NO_SHADE | RT_FLAG_NO_TRACE)) &&
+        const bool want = cam && !dup &&
+                          !(flags & (RT_FLAG_STAMPS | RT_FLAG_NO_SHADE | RT_FLAG_NO_TRACE | RT_FLAG_GENERATIONS)) &&
                           (ctx->jit_mode == RT_JIT_SYNC || (ctx->jit_mode >= RT_JIT_AUTO && P.n_tiles >= kJitMinTiles));
         if (want) ++ctx->jit_frames;
         if (want && (rc = jit_function(ctx, ls.pool, ls.world_lds != 0, ls.lds, ls.per_cu, &jf))) return rc;
@@ -740,12 +744,26 @@ int copy_to_host(rt_context* ctx, void* out, size_t bytes) {
     return RT_OK;
 }
 
+// The kernels' error word (LaunchParams::error_flag bits, rtc_internal.hpp).
+std::string device_error_text(int32_t err) {
+    std::string m;
+    auto add = [&](int32_t bit, const char* what) {
+        if (err & bit) m += (m.empty() ? "" : "; ") + std::string(what);
+    };
+    add(kErrPoolOverflow, "device ray pool overflow");
+    add(kErrBoundsSlot, "bounds check: pool slot outside the LIFO bound");
+    add(kErrBoundsSpill, "bounds check: spill region outside the spill buffer");
+    add(kErrBoundsTile, "bounds check: work item tile outside the launch");
+    add(kErrBoundsOut, "bounds check: output index outside the canvas");
+    return m.empty() ? "device error " + std::to_string(err) : m;
+}
+
 int check_pool_error(rt_context* ctx) {
     int32_t err = 0;
     RT_HIP(hipMemcpy(&err, ctx->d_error, sizeof(err), hipMemcpyDeviceToHost));
     if (err) {
         RT_HIP(hipMemset(ctx->d_error, 0, sizeof(int32_t)));
-        return set_error(RT_ERR_POOL, "device ray pool overflow");
+        return set_error(RT_ERR_POOL, device_error_text(err));
     }
     return RT_OK;
 }
@@ -850,6 +868,9 @@ int create_device_context(int device_ordinal, rt_context** out) {
     RT_HIP(hipMemset(ctx->d_counters, 0, counter_bytes));
     RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_error), sizeof(int32_t)));
     RT_HIP(hipMemset(ctx->d_error, 0, sizeof(int32_t)));
+    const size_t gen_bytes = 2 * (size_t)kGenSlots * sizeof(unsigned long long);
+    RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_gen_counts), gen_bytes));
+    RT_HIP(hipMemset(ctx->d_gen_counts, 0, gen_bytes));
     *out = ctx.release();
     return RT_OK;
 }
@@ -863,6 +884,7 @@ void destroy_device_context(rt_context* ctx) {
     (void)hipFree(ctx->d_tile_counter);
     (void)hipFree(ctx->d_counters);
     (void)hipFree(ctx->d_error);
+    (void)hipFree(ctx->d_gen_counts);
     (void)hipFree(ctx->d_scratch);
     (void)hipFree(ctx->d_stamps);
     (void)hipFree(ctx->d_item_log);
@@ -1034,7 +1056,7 @@ int rt_render(rt_context* ctx, const rt_camera_desc* cam, const rt_render_option
     RT_HIP(hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_stop));
     if (*h_err) {
         RT_HIP(hipMemset(ctx->d_error, 0, sizeof(int32_t)));
-        return set_error(RT_ERR_POOL, "device ray pool overflow");
+        return set_error(RT_ERR_POOL, device_error_text(*h_err));
     }
     if (stats) {
         unsigned long long before[kNumCounters] = {}, after[kNumCounters] = {};
@@ -1155,12 +1177,19 @@ int rt_jit_status(rt_context* ctx, int* used_last_launch, double* compile_ms, ch
 
 int rt_jit_wait(rt_context* ctx, double timeout_ms, int* pending) {
     if (!ctx) return set_error(RT_ERR_INVALID, "null context");
+    // one deadline for the whole group: each member waits for what is left of it
+    const auto t0 = std::chrono::steady_clock::now();
+    auto remaining = [&] {
+        if (timeout_ms < 0) return timeout_ms;
+        const double spent = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return std::max(0.0, timeout_ms - spent);
+    };
     int total = 0, left = 0;
     for (rt_context* c : ctx->peers) {
-        jit_wait(c, timeout_ms, &left);
+        jit_wait(c, remaining(), &left);
         total += left;
     }
-    jit_wait(ctx, timeout_ms, &left);
+    jit_wait(ctx, remaining(), &left);
     if (pending) *pending = total + left;
     return RT_OK;
 }
@@ -1209,6 +1238,25 @@ int rt_read_counters(rt_context* ctx, rt_stats* totals) {
     if (rc) return rc;
     fill_stats(ctx, zero, now, 0.f, totals);
     return check_pool_error(ctx);
+}
+
+int rt_read_generation_counts(rt_context* ctx, rt_generation_counts* out) {
+    if (!ctx || !out) return set_error(RT_ERR_INVALID, "null argument");
+    std::memset(out, 0, sizeof(*out));
+    std::vector<rt_context*> members = {ctx};
+    members.insert(members.end(), ctx->peers.begin(), ctx->peers.end());
+    for (rt_context* m : members) {
+        unsigned long long buf[2 * kGenSlots];
+        RT_HIP(hipSetDevice(m->device));
+        RT_HIP(hipDeviceSynchronize());
+        RT_HIP(hipMemcpy(buf, m->d_gen_counts, sizeof buf, hipMemcpyDeviceToHost));
+        for (int i = 0; i < kGenSlots; ++i) {
+            out->traced[i] += buf[i];
+            out->shaded[i] += buf[kGenSlots + i];
+        }
+    }
+    RT_HIP(hipSetDevice(ctx->device));
+    return RT_OK;
 }
 
 int rt_assemble_shards(rt_context* ctx, const void* gathered, uint32_t width, uint32_t height, uint32_t shards,

@@ -56,6 +56,7 @@ constexpr int kTilePixels = RT_TILE_W * RT_TILE_H;  // one tile per workgroup pa
 static_assert(kTilePixels == kBlock, "one pixel per thread per tile");
 constexpr int kNumKinds = 6;
 constexpr int kNumCounters = 8;    // order of rt_stats' first eight fields
+constexpr int kGenSlots = RT_MAX_SUPPORTED_DEPTH + 1;  // rt_generation_counts, by `remaining`
 // Event counters are sharded: workgroup b adds into shard b % kCounterShards
 // (same-address global atomics from every workgroup cost ~66 us per 1080p
 // frame on MI355X; sharded they are noise).  The host sums the shards.
@@ -82,6 +83,46 @@ constexpr uint32_t kItemTileMask = 0xFFFFFu;
 constexpr uint32_t kItemPartShift = 20, kItemSplitShift = 24, kItemPartMask = 15u, kItemSplitMask = 7u;
 constexpr uint32_t kItemPrioShift = 27;
 constexpr uint32_t kMaxSplitLog2 = 4;  // up to 16 items per tile
+constexpr uint32_t kNoItem = 0xFFFFFFFFu;  // next_tile: the launch's items are all taken
+
+// A work item, decoded.  Only launches that hand items out through a tile
+// order (LaunchParams::tile_order set: cost-ordered or centre-out, which
+// plan_tile_order allows for n_tiles <= 2^20 only) carry the packed fields;
+// a raster launch's item is the plain tile index, whatever the launch's size
+// (an rt_color_at batch reaches 2^24 tiles).  Decoding a raster item >= 2^20
+// as packed would mask its tile and read stray part/split/priority bits.
+struct WorkItem {
+    uint32_t tile, part, split_log2, prio;
+};
+RTC_HD inline WorkItem decode_item(uint32_t item, bool packed) {
+    if (!packed) return {item, 0u, 0u, 0u};
+    return {item & kItemTileMask, (item >> kItemPartShift) & kItemPartMask, (item >> kItemSplitShift) & kItemSplitMask,
+            (item >> kItemPrioShift) & 3u};
+}
+RTC_HD inline uint32_t encode_item(uint32_t tile, uint32_t part, uint32_t split_log2, uint32_t prio) {
+    return tile | part << kItemPartShift | split_log2 << kItemSplitShift | prio << kItemPrioShift;
+}
+// Part p of a tile split 2^l ways seeds the threads t of the tile's
+// workgroup with t >> (8 - l) == p (halves, wave pairs, waves, half-waves,
+// wave rows); l = 0 seeds all 256.
+RTC_HD inline bool item_seeds(uint32_t tid, const WorkItem& w) { return (tid >> (8u - w.split_log2)) == w.part; }
+
+// Spilled pool entries: workgroup b of a pool launch owns records
+// [b * spill_cap, (b + 1) * spill_cap) of LaunchParams::spill, 8 words each;
+// slot s >= lds_cap of its LIFO is record s - lds_cap.
+RTC_HD inline uint64_t spill_word(uint32_t block, uint32_t spill_cap, uint32_t slot, uint32_t lds_cap) {
+    return ((uint64_t)block * spill_cap + (slot - lds_cap)) * 8u;
+}
+
+// RTC_BOUNDS_CHECK builds (debug variant, scripts/build_variant.sh): the pool
+// kernel checks every computed index against its buffer before the access,
+// skips a bad access and raises one of these bits of LaunchParams::error_flag
+// (the host reports them as RT_ERR_POOL with the bit's name).
+constexpr int32_t kErrPoolOverflow = 1;  // a child beyond the LIFO bound (no debug build needed)
+constexpr int32_t kErrBoundsSlot = 4;    // pool slot outside [0, cap)
+constexpr int32_t kErrBoundsSpill = 8;   // spill record outside the launch's spill buffer
+constexpr int32_t kErrBoundsTile = 16;   // work item's tile >= n_tiles
+constexpr int32_t kErrBoundsOut = 32;    // output element outside the canvas or strip
 // Tile scheduling modes (RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic)
 constexpr uint32_t kSchedGrid = 0;     // one workgroup per tile; the dispatcher balances
 constexpr uint32_t kSchedDynamic = 1;  // resident grid, per-XCD atomic tile queues
@@ -207,6 +248,8 @@ struct LaunchParams {
     uint32_t flags;          // RT_FLAG_* diagnostic ablations
     uint32_t world_lds;      // bytes of world tables staged at the start of dynamic LDS (0 = none)
     void* spill;                 // pool overflow: grid x 8 x (pool_capacity - pool_lds_capacity) words
+    uint32_t spill_blocks;       // workgroups the spill buffer holds regions for (RTC_BOUNDS_CHECK)
+    uint32_t pad_spill;
     unsigned long long* stamps;  // RT_FLAG_STAMPS: 2 x grid s_memrealtime values
     unsigned long long* item_log;  // RT_FLAG_STAMPS pool launches: [0] count, then 3 x u64 per item
     unsigned long long* tile_counter;  // kTileQueues queue heads, kQueueStride apart (zero at launch)
@@ -215,6 +258,7 @@ struct LaunchParams {
     const uint32_t* item_count;        // items in tile_order (>= n_tiles: split tiles), null = n_tiles
     uint32_t* tile_cost;               // pool kernel: per-tile duration (10 ns ticks), null = not recorded
     unsigned long long* counters;      // kCounterShards x kNumCounters cumulative u64
+    unsigned long long* gen_counts;    // RT_FLAG_GENERATIONS: traced[kGenSlots], shaded[kGenSlots]; else null
     int32_t* error_flag;               // set nonzero on pool overflow
 };
 

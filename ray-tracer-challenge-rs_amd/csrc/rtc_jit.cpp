@@ -380,6 +380,9 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
         table = fnv(ctx->jit_lights.data(), ctx->jit_lights.size() * sizeof(LightRec<float>), table);
         const uint32_t traits[3] = {ctx->jit_patterns, ctx->jit_pattern_kinds, ctx->jit_transparent};
         table = fnv(traits, sizeof traits, table);
+        // the device's gfx target: each build is compiled for one (make_request),
+        // so devices of another target in the same process get builds of their own
+        table = fnv(ctx->arch.data(), ctx->arch.size() + 1, table);
         const uint32_t start_at = ctx->jit_mode == RT_JIT_AUTO ? 2 : 1;
         bool start = false;
         {

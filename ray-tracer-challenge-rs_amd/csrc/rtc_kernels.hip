@@ -941,6 +941,24 @@ struct NoPush {
     __device__ void operator()(V, V, R) const {}
 };
 
+// RT_FLAG_GENERATIONS (generic kernels only; a diagnostic frame, e.g. the
+// bench's per-generation line): the wave's traced rays and shaded hits by
+// `remaining`, one pass per distinct value among the traced lanes and one
+// global atomic pair per pass from lane 0.  Call where every lane arrives.
+__device__ inline void count_generations(unsigned long long* gc, bool traced, bool shaded, uint32_t rem) {
+    unsigned long long left = __builtin_amdgcn_ballot_w64(traced);
+    while (left) {
+        const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)rem, (int)__builtin_ctzll(left));
+        const unsigned long long same = __builtin_amdgcn_ballot_w64(traced && rem == r);
+        const unsigned long long hit = __builtin_amdgcn_ballot_w64(shaded && rem == r);
+        if ((threadIdx.x & 63) == 0 && r < (uint32_t)kGenSlots) {
+            atomicAdd(&gc[r], (unsigned long long)__builtin_popcountll(same));
+            if (hit) atomicAdd(&gc[kGenSlots + r], (unsigned long long)__builtin_popcountll(hit));
+        }
+        left &= ~same;
+    }
+}
+
 // Count one wave's events after shading (call where every lane arrives):
 // `primary` rays entering the path, `hit` = shade_ray's result.
 template <typename R>
@@ -1227,10 +1245,10 @@ __device__ inline void flush_counts(const Counts& k, unsigned long long* global)
 // need no other bookkeeping.
 template <typename R>
 __device__ inline unsigned int next_tile(const LaunchParams<R>& P, uint32_t it, uint32_t& probe, uint32_t n_items) {
-    if (P.persistent == kSchedGrid) return it == 0 ? blockIdx.x : 0xFFFFFFFFu;
+    if (P.persistent == kSchedGrid) return it == 0 ? blockIdx.x : kNoItem;
     if (P.persistent == kSchedStatic) {
         const unsigned long long t = blockIdx.x + (unsigned long long)it * gridDim.x;
-        return t < P.n_tiles ? (unsigned int)t : 0xFFFFFFFFu;
+        return t < P.n_tiles ? (unsigned int)t : kNoItem;
     }
     for (; probe < (uint32_t)kTileQueues; ++probe) {
         const uint32_t q = (blockIdx.x + probe) % kTileQueues;
@@ -1238,7 +1256,7 @@ __device__ inline unsigned int next_tile(const LaunchParams<R>& P, uint32_t it, 
         const unsigned long long i = q + (unsigned long long)kTileQueues * j;
         if (i < n_items) return P.tile_order ? P.tile_order[i] : (unsigned int)i;
     }
-    return 0xFFFFFFFFu;
+    return kNoItem;
 }
 
 // The world as seen by one launch, rebuilt from the restrict parameters.
@@ -1373,6 +1391,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
             }
         }
         count_events(k, valid, hit, sh, sc.n_lights);
+        if (kDiag && P.gen_counts) count_generations(P.gen_counts, valid, hit, P.max_depth);
         if (valid) store_pixel(P, out_idx, c);
     }
     if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
@@ -1404,7 +1423,25 @@ struct Pool {
     R* lds;    // 8 arrays of lds_cap words: ox oy oz dx dy dz w, then meta (u32)
     R* spill;  // spill_cap records of 8 words (this workgroup's region)
     int lds_cap, spill_cap;
+#ifdef RTC_BOUNDS_CHECK
+    int32_t* err;  // LaunchParams::error_flag
+#endif
 };
+
+// RTC_BOUNDS_CHECK (debug builds): false, with the bit raised, when an index
+// is outside its buffer; the caller then skips the access.  Product builds
+// compile the checks out.
+__device__ inline bool in_bounds(bool ok, int32_t* err, int32_t bit) {
+#ifdef RTC_BOUNDS_CHECK
+    if (!ok) atomicOr(err, bit);
+    return ok;
+#else
+    (void)err;
+    (void)bit;
+    (void)ok;
+    return true;
+#endif
+}
 
 // Reserve `pred` slots for the lanes of one wave: ballot + mbcnt prefix, one
 // LDS atomic per wave.  Returns the lane's slot or -1.
@@ -1488,6 +1525,9 @@ __device__ inline void spill_load(const RTC_AS_GLOBAL R* e, V3<R>& o, V3<R>& d, 
 
 template <typename R>
 __device__ inline void pool_put(const Pool<R>& pl, int slot, V3<R> o, V3<R> d, R w, uint32_t meta) {
+#ifdef RTC_BOUNDS_CHECK
+    if (!in_bounds(slot >= 0 && slot < pl.lds_cap + pl.spill_cap, pl.err, kErrBoundsSlot)) return;
+#endif
     if (slot < pl.lds_cap) {
         RTC_AS_LDS R* b = (RTC_AS_LDS R*)pl.lds;
         pool_store<R>(b, (RTC_AS_LDS uint32_t*)(b + 7 * pl.lds_cap), pl.lds_cap, slot, o, d, w, meta);
@@ -1498,6 +1538,14 @@ __device__ inline void pool_put(const Pool<R>& pl, int slot, V3<R> o, V3<R> d, R
 
 template <typename R>
 __device__ inline void pool_get(const Pool<R>& pl, int slot, V3<R>& o, V3<R>& d, R& w, uint32_t& meta) {
+#ifdef RTC_BOUNDS_CHECK
+    if (!in_bounds(slot >= 0 && slot < pl.lds_cap + pl.spill_cap, pl.err, kErrBoundsSlot)) {
+        o = d = {(R)0, (R)0, (R)0};
+        w = (R)0;
+        meta = 0;
+        return;
+    }
+#endif
     if (slot < pl.lds_cap) {
         const RTC_AS_LDS R* b = (const RTC_AS_LDS R*)pl.lds;
         pool_load<R>(b, (const RTC_AS_LDS uint32_t*)(b + 7 * pl.lds_cap), pl.lds_cap, slot, o, d, w, meta);
@@ -1530,8 +1578,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     pl.lds = reinterpret_cast<R*>(smem + 3 * kBlock * sizeof(long long));
     pl.lds_cap = (int)lcap;
     // 8 words per spilled entry; blockIdx.x < grid (persistent launch)
-    pl.spill = reinterpret_cast<R*>(P.spill) + (size_t)blockIdx.x * 8 * gcap;
+    pl.spill = reinterpret_cast<R*>(P.spill) + spill_word(blockIdx.x, gcap, lcap, lcap);
     pl.spill_cap = (int)gcap;
+#ifdef RTC_BOUNDS_CHECK
+    pl.err = P.error_flag;
+    if (!in_bounds(gcap == 0 || blockIdx.x < P.spill_blocks, P.error_flag, kErrBoundsSpill)) pl.spill_cap = 0;
+#endif
 
     Counts k = {};
     const uint32_t tid = threadIdx.x;
@@ -1553,18 +1605,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         for (int c = 0; c < 3; ++c) pl.acc[c * kBlock + tid] = 0;
         __syncthreads();
         const uint32_t item = __builtin_amdgcn_readfirstlane(s_tile[it & 1]);
-        if (item == 0xFFFFFFFFu) break;
-        const uint32_t t = item & kItemTileMask, split = (item >> kItemSplitShift) & kItemSplitMask;
+        if (item == kNoItem) break;
+        // packed fields only in items handed out through a tile order (raster
+        // items are plain tile indices, any number of them)
+        const WorkItem wi = decode_item(item, P.tile_order != nullptr);
+        const uint32_t t = wi.tile, split = wi.split_log2;
+#ifdef RTC_BOUNDS_CHECK
+        if (!in_bounds(t < P.n_tiles, P.error_flag, kErrBoundsTile)) continue;  // (every thread: uniform)
+#endif
         // the costliest items set the launch's tail: their waves win issue
         // arbitration against the other workgroups' on the same SIMDs
-        const uint32_t prio = (item >> kItemPrioShift) & 3u;
+        const uint32_t prio = wi.prio;
         if (prio) set_wave_prio(prio);
         bool valid;
         V3<R> o, d;
         uint64_t out_idx;
         load_primary(P, t, tid, valid, o, d, out_idx);
         // this item's part of the tile (all of it unless split)
-        valid &= (tid >> (8 - split)) == ((item >> kItemPartShift) & kItemPartMask);
+        valid &= item_seeds(tid, wi);
         k.c[0] += wave_count(valid);
         {
             const int slot = wave_reserve(valid, &s_top[0]);
@@ -1593,10 +1651,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
             auto push = [&](V3<R> co, V3<R> cd, R cw) {
                 const int slot = wave_reserve(true, &s_top[cur ^ 1]);
                 if (slot < (int)cap) pool_put(pl, slot, co, cd, rw * cw, child_meta);
-                else atomicOr(P.error_flag, 1);
+                else atomicOr(P.error_flag, kErrPoolOverflow);
             };
             if (active) hit = shade_ray<R, true, kDup>(sc, ro, rd, meta >> 8, sh, push);
             count_events(k, false, hit, sh, sc.n_lights);
+#ifndef RTC_JIT  // (per-scene builds never take RT_FLAG_GENERATIONS launches)
+            if (P.gen_counts) count_generations(P.gen_counts, active, hit, meta >> 8);
+#endif
             if (hit) {
                 acc_add(pl.acc, pix, (double)(sh.surface.x * rw));
                 acc_add(pl.acc + kBlock, pix, (double)(sh.surface.y * rw));
@@ -1611,6 +1672,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         }
         const V3<R> c = {(R)((double)pl.acc[tid] * kAccInvScale), (R)((double)pl.acc[kBlock + tid] * kAccInvScale),
                          (R)((double)pl.acc[2 * kBlock + tid] * kAccInvScale)};
+#ifdef RTC_BOUNDS_CHECK
+        valid &= in_bounds(!valid || out_idx < (P.rays ? P.n_rays : (uint64_t)P.tile_rows * RT_TILE_H * P.width),
+                           P.error_flag, kErrBoundsOut);
+#endif
         if (valid) store_pixel(P, out_idx, c);
         if (prio) __builtin_amdgcn_s_setprio(0);
         __syncthreads();  // accumulators are re-zeroed for the next tile
@@ -1768,9 +1833,7 @@ __global__ __launch_bounds__(kOrderThreads) void order_tiles(uint32_t* __restric
         // priority: 3 above the urgent cost, or graded 1/2/3 above 1x/2x/4x it
         const float pc = (float)(c >> l);
         const uint32_t pr = !(pc > urgent) ? 0u : !graded ? 3u : pc > 4.0f * urgent ? 3u : pc > 2.0f * urgent ? 2u : 1u;
-        const uint32_t flag = pr << kItemPrioShift;
-        for (uint32_t p = 0; p < (1u << l); ++p)
-            order[pos + p] = i | p << kItemPartShift | l << kItemSplitShift | flag;
+        for (uint32_t p = 0; p < (1u << l); ++p) order[pos + p] = encode_item(i, p, l, pr);
         if (l) cost[i] = 0;
     }
     if (threadIdx.x == 0) *n_items = items;

@@ -46,6 +46,7 @@ PATTERN_KINDS = {"stripe": 0, "gradient": 1, "ring": 2, "checker": 3, "complex":
 PRECISIONS = {"f32": 0, "f64": 1}
 # rt_render_options.flags: diagnostic ablations (rtc.h); never in a parity or bench result
 RT_FLAG_NO_COUNTERS, RT_FLAG_NO_SHADE, RT_FLAG_NO_TRACE, RT_FLAG_STAMPS, RT_FLAG_FAIL_LAUNCH = 1, 2, 4, 8, 16
+RT_FLAG_GENERATIONS = 32  # count rays per generation (rt_read_generation_counts); pixels unchanged
 RT_JIT_OFF, RT_JIT_SYNC, RT_JIT_AUTO, RT_JIT_EAGER = 0, 1, 2, 3
 OUT_FORMATS = {"real": 0, "u8": 1}
 
@@ -109,6 +110,11 @@ class Stats(C.Structure):
         return d
 
 
+class GenerationCounts(C.Structure):
+    _fields_ = [("traced", C.c_uint64 * (RT_MAX_SUPPORTED_DEPTH + 1)),
+                ("shaded", C.c_uint64 * (RT_MAX_SUPPORTED_DEPTH + 1))]
+
+
 class SceneView(C.Structure):
     _fields_ = [("shapes", C.POINTER(ShapeDesc)), ("n_shapes", C.c_uint32),
                 ("materials", C.POINTER(MaterialDesc)), ("n_materials", C.c_uint32),
@@ -137,10 +143,14 @@ def _load() -> C.CDLL:
     # arguments then hits HBM/L2 instead of crossing PCIe (measured ~2 us per
     # 1080p frame on MI355X).  Must be set before the HIP runtime starts.
     os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # RTC_NO_TORCH=1: a torch-free host (bench.py's one-shot child, timing
+    # what a Rust caller of the C-ABI pays: the HIP runtime starts in
+    # rt_context_create); librtc then binds /opt/rocm's runtime on its own.
+    if os.environ.get("RTC_NO_TORCH") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     if not os.path.exists(path):
         raise ImportError(f"rtc_amd: {path} is missing — build it with `python -c 'import __graft_entry__ as g; "
                           f"g.build()'` (hipcc --offload-arch=gfx950)")
@@ -160,6 +170,7 @@ def _load() -> C.CDLL:
         "rt_color_at": (C.c_int, [C.c_void_p, P(C.c_double), C.c_uint64, C.c_uint32, C.c_uint32, P(C.c_double),
                                   P(Stats)]),
         "rt_read_counters": (C.c_int, [C.c_void_p, P(Stats)]),
+        "rt_read_generation_counts": (C.c_int, [C.c_void_p, P(GenerationCounts)]),
         "rt_debug_stamps": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_uint32, P(C.c_uint32)]),
         "rt_debug_tile_costs": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_uint32, P(C.c_uint32)]),
         "rt_debug_item_log": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_uint32, P(C.c_uint32)]),
@@ -205,6 +216,7 @@ _lib = _load()
 EXPORTED_SYMBOLS = (
     "rt_abi_version", "rt_last_error", "rt_device_count", "rt_context_create", "rt_context_destroy",
     "rt_scene_upload", "rt_shard_rows", "rt_render", "rt_render_device", "rt_color_at", "rt_read_counters",
+    "rt_read_generation_counts",
     "rt_debug_stamps", "rt_debug_tile_costs", "rt_debug_item_log", "rt_debug_intersect", "rt_debug_normal", "rt_camera_set_transform",
     "rt_shard_row_map", "rt_context_create_multi", "rt_comm_unique_id", "rt_context_create_rank", "rt_context_group",
     "rt_context_set_jit", "rt_jit_status", "rt_jit_wait",
@@ -533,6 +545,25 @@ class Context:
         st = Stats()
         _check(_lib.rt_read_counters(self._h, C.byref(st)))
         return st.as_dict()
+
+    def generation_counts(self):
+        """(traced, shaded) per `remaining` 0..16, cumulative over RT_FLAG_GENERATIONS launches (rtc.h)."""
+        g = GenerationCounts()
+        _check(_lib.rt_read_generation_counts(self._h, C.byref(g)))
+        return np.array(g.traced[:], dtype=np.uint64), np.array(g.shaded[:], dtype=np.uint64)
+
+    def render_generations(self, camera: CameraDesc, depth: int = RT_DEFAULT_MAX_DEPTH, precision: str = "f32"):
+        """One diagnostic frame with RT_FLAG_GENERATIONS: (image, stats, per-generation dict).  Generation g
+        (0 = camera rays) is `remaining` depth - g; shadow rays are L per shaded hit (world.rs:46-52)."""
+        t0, s0 = self.generation_counts()
+        opts = self.options(depth, precision, "real", (0, 1), RT_FLAG_GENERATIONS)
+        dtype = np.float32 if precision == "f32" else np.float64
+        img = np.zeros((camera.height, camera.width, 3), dtype=dtype)
+        st = Stats()
+        _check(_lib.rt_render(self._h, C.byref(camera), C.byref(opts), img.ctypes.data_as(C.c_void_p), C.byref(st)))
+        t1, s1 = self.generation_counts()
+        traced, shaded = (t1 - t0)[::-1][-(depth + 1):], (s1 - s0)[::-1][-(depth + 1):]
+        return img, st.as_dict(), {"traced": [int(v) for v in traced], "shaded": [int(v) for v in shaded]}
 
     def assemble_shards(self, gathered_ptr: int, width: int, height: int, shards: int, bytes_per_pixel: int,
                         image_ptr: int, stream_ptr: int | None = None) -> None:

@@ -1,0 +1,51 @@
+#!/bin/bash
+# One gpurun session, steps chosen by name (each with its own time limit; a
+# crash or timeout, rc other than 0/1, ends the session):
+#   tests    pytest -m gpu (whole suite)            -> gpurun_out/pytest_gpu.log
+#   bctests  the same suite on the RTC_BOUNDS_CHECK build (_lib_bc)
+#   smoke    __graft_entry__.smoke()
+#   bench    bench.py with the driver's flags, then 1000 steps; f64 line
+#   pool     bench lines of the pool configs (reflect_refract, cover/table 4K)
+#   prof     rocprofv3 --kernel-trace --stats of the bench     -> gpurun_out/prof_*
+# Usage: scripts/gpu_session.sh tests smoke bench ...
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+L=$PWD/ray-tracer-challenge-rs_amd/rtc_amd
+ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+        > gpurun_out/pytest_gpu.log 2>&1
+      rc=$?; echo "tests rc=$rc"; tail -15 gpurun_out/pytest_gpu.log; ok $rc || exit $rc ;;
+    bctests)
+      RTC_LIBRARY=$L/_lib_bc/librtc.so RTC_JIT_CACHE=0 timeout -k 10 600 python -u -m pytest tests -m gpu -q \
+        --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu_bc.log 2>&1
+      rc=$?; echo "bctests rc=$rc"; tail -15 gpurun_out/pytest_gpu_bc.log; ok $rc || exit $rc ;;
+    smoke)
+      timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+      rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log; ok $rc || exit $rc ;;
+    bench)
+      timeout -k 10 240 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_driver.log 2>&1
+      rc=$?; echo "bench(driver flags) rc=$rc"; tail -c 3000 gpurun_out/bench_driver.log; echo; [ $rc -eq 0 ] || exit $rc
+      timeout -k 10 240 python bench.py --no-cpu-baseline > gpurun_out/bench_1000.log 2>&1
+      rc=$?; echo "bench(1000) rc=$rc"; tail -c 1500 gpurun_out/bench_1000.log; echo; [ $rc -eq 0 ] || exit $rc ;;
+    pool)
+      : > gpurun_out/bench_pool.log
+      for a in "--scene reflect_refract" "--scene cover --width 3840 --height 2160 --steps 300" \
+               "--scene table --width 3840 --height 2160 --steps 300"; do
+        timeout -k 10 240 python bench.py $a --no-cpu-baseline >> gpurun_out/bench_pool.log 2>&1
+        rc=$?; echo "pool $a rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      done
+      tail -c 2000 gpurun_out/bench_pool.log; echo ;;
+    prof)
+      for sc in three_sphere_scene reflect_refract; do
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$sc -o run -- \
+          python3 bench.py --scene $sc --steps 200 --warmup 10 --no-cpu-baseline > gpurun_out/prof_$sc.log 2>&1
+        rc=$?; echo "prof $sc rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      done ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

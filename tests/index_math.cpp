@@ -1,0 +1,85 @@
+// index_math.cpp — CPU check of the pool kernel's index arithmetic
+// (rtc_internal.hpp, shared with rtc_kernels.hip): work-item encoding and
+// decoding, the threads a split part seeds, spill addressing and the
+// row-block shard maps.  Built with g++ by tests/test_index_math.py; prints
+// "ok" or the first failure.
+#include <cstdio>
+#include <cstdlib>
+#include <set>
+
+#include "../ray-tracer-challenge-rs_amd/csrc/rtc_internal.hpp"
+
+using namespace rtc;
+
+#define CHECK(c)                                                      \
+    do {                                                              \
+        if (!(c)) {                                                   \
+            std::printf("FAIL %s:%d: %s\n", __FILE__, __LINE__, #c);  \
+            return 1;                                                 \
+        }                                                             \
+    } while (0)
+
+int main() {
+    // packed items round-trip for every field value a tile order can hold
+    for (uint32_t l = 0; l <= kMaxSplitLog2; ++l)
+        for (uint32_t p = 0; p < (1u << l); ++p)
+            for (uint32_t pr = 0; pr < 4; ++pr)
+                for (uint32_t t : {0u, 1u, 4095u, 32399u, 0x7FFFFu, kItemTileMask}) {
+                    const uint32_t item = encode_item(t, p, l, pr);
+                    CHECK(item != kNoItem);
+                    const WorkItem w = decode_item(item, true);
+                    CHECK(w.tile == t && w.part == p && w.split_log2 == l && w.prio == pr);
+                }
+    // raster items are plain tiles at every size (rt_color_at: up to 2^24 tiles)
+    for (uint32_t t : {0u, kItemTileMask, kItemTileMask + 1u, 0x1234567u, 0xFFFFFFu, 0xFFFFFFFEu}) {
+        const WorkItem w = decode_item(t, false);
+        CHECK(w.tile == t && w.part == 0 && w.split_log2 == 0 && w.prio == 0);
+        int seeded = 0;
+        for (uint32_t tid = 0; tid < (uint32_t)kBlock; ++tid) seeded += item_seeds(tid, w);
+        CHECK(seeded == kBlock);  // an unsplit item seeds the whole tile
+    }
+    // the parts of a split tile partition its threads into equal runs
+    for (uint32_t l = 0; l <= kMaxSplitLog2; ++l) {
+        std::set<uint32_t> seen;
+        for (uint32_t p = 0; p < (1u << l); ++p) {
+            const WorkItem w = decode_item(encode_item(7, p, l, 0), true);
+            int n = 0;
+            for (uint32_t tid = 0; tid < (uint32_t)kBlock; ++tid)
+                if (item_seeds(tid, w)) {
+                    CHECK(seen.insert(tid).second);
+                    ++n;
+                }
+            CHECK(n == (kBlock >> l));
+        }
+        CHECK((int)seen.size() == kBlock);
+    }
+    // spill records: workgroup b's slots [lcap, cap) map to its own run of
+    // records, inside grid * (cap - lcap) records
+    for (uint32_t grid : {1u, 7u, 1536u})
+        for (uint32_t lcap : {256u, 320u, 512u})
+            for (uint32_t depth : {1u, 6u, 16u}) {
+                const uint32_t cap = kBlock + depth * kBlock;
+                if (cap <= lcap) continue;
+                const uint32_t gcap = cap - lcap;
+                const uint64_t words = (uint64_t)grid * gcap * 8;
+                for (uint32_t b : {0u, grid / 2, grid - 1}) {
+                    const uint64_t lo = spill_word(b, gcap, lcap, lcap), hi = spill_word(b, gcap, cap - 1, lcap);
+                    CHECK(lo == (uint64_t)b * gcap * 8);
+                    CHECK(hi + 8 <= words && hi + 8 == lo + (uint64_t)gcap * 8);
+                }
+            }
+    // row-block shards: every image row has one (shard, strip row), inside
+    // that shard's strip, and the map inverts
+    for (uint32_t h : {1u, 7u, 1080u, 2160u, 2161u})
+        for (uint32_t n : {1u, 2u, 3u, 8u}) {
+            const uint32_t rows = shard_tile_rows(h, n, 0) * RT_TILE_H;
+            for (uint32_t y = 0; y < h; ++y) {
+                uint32_t s, r;
+                shard_of_image_row(y, n, &s, &r);
+                CHECK(s < n && r < shard_tile_rows(h, n, s) * RT_TILE_H && r < rows);
+                CHECK(shard_image_row(r, n, s) == y);
+            }
+        }
+    std::printf("ok\n");
+    return 0;
+}

@@ -3,10 +3,14 @@
   configs[0]  three_sphere_scene 320x240   against the oracle's SERIAL
               Camera::render (camera.rs:79-95): f64 within 1e-9 with equal
               counters, the u8 canvas, f32
-  configs[1]  three_sphere_scene 1920x1080 (tests/test_gpu_parity.py)
+  configs[1]  three_sphere_scene 1920x1080 depth 5, the bench's own kernel
   configs[2]  reflect_refract   1920x1080  (f32 and f64)
   configs[3]  cover             3840x2160  (f32 and f64; + the 8-shard split)
   configs[4]  table             3840x2160  (f32 and f64)
+
+Every f32 frame here runs twice: on the generic kernel and on the per-scene
+hipRTC build (RT_JIT_SYNC) that bench.py times at these sizes; the two must
+agree bit for bit, and the per-scene frame is the one held to the tolerance.
 
 Tolerances are the suite's (tests/test_gpu_parity.py): f64 every pixel within
 1e-9 and all eight counters identical; f32 at least 99 % of pixels within
@@ -74,11 +78,31 @@ def test_config_full_size_f64(gpu_ctx, oracle, rtc, name):
     assert _counts(st) == _counts(rst)
 
 
-@pytest.mark.parametrize("name", list(CONFIGS))
-def test_config_full_size_f32(gpu_ctx, oracle, rtc, name):
-    scene, cam, ref, rst = _oracle_frame(oracle, rtc, name)
-    gpu_ctx.upload(scene)
-    img, st = gpu_ctx.render(cam, 6, precision="f32")
+def _generic_and_per_scene(gpu_ctx, rtc, cam, depth):
+    """The f32 frame from the generic kernel (RT_JIT_OFF) and from the
+    per-scene hipRTC build (RT_JIT_SYNC: built in line), which is the code
+    object bench.py times (it waits for the same build before its warm-up);
+    asserts the per-scene kernel really ran."""
+    try:
+        gpu_ctx.set_jit(rtc.RT_JIT_OFF)
+        generic, gst = gpu_ctx.render(cam, depth, precision="f32")
+        assert not gpu_ctx.jit_status()["used"]
+        gpu_ctx.set_jit(rtc.RT_JIT_SYNC)
+        img, st = gpu_ctx.render(cam, depth, precision="f32")
+        js = gpu_ctx.jit_status()
+        assert js["used"], f"the per-scene kernel did not run: {js['log'][:400]}"
+        # a repeated launch (cost-ordered for pool scenes) reproduces it bit for bit
+        img2, st2 = gpu_ctx.render(cam, depth, precision="f32")
+        assert gpu_ctx.jit_status()["used"]
+    finally:
+        gpu_ctx.set_jit(rtc.RT_JIT_AUTO)
+    assert np.array_equal(img, generic), f"{int((img != generic).any(axis=2).sum())} px differ from the generic kernel"
+    assert _counts(st) == _counts(gst)
+    assert np.array_equal(img, img2) and _counts(st) == _counts(st2)
+    return img, st
+
+
+def _f32_tolerance(name, oracle, img, st, ref, rst):
     d = np.abs(oracle.quantize(img).astype(np.int16) - oracle.quantize(ref).astype(np.int16)).max(axis=2)
     agree = float((d <= 2).mean())
     mean = float(np.abs(img.astype(np.float64) - ref).mean())
@@ -87,9 +111,32 @@ def test_config_full_size_f32(gpu_ctx, oracle, rtc, name):
     assert abs(st["rays"] - rst["rays"]) <= 0.01 * rst["rays"], (st["rays"], rst["rays"])
     for k in ("primary", "shadow", "reflect", "refract"):
         assert abs(st[k] - rst[k]) <= 0.05 * max(20, rst[k]), (k, st[k], rst[k])
-    # repeated launches (the second cost-ordered) reproduce the frame bit for bit
-    img2, st2 = gpu_ctx.render(cam, 6, precision="f32")
-    assert np.array_equal(img, img2) and _counts(st) == _counts(st2)
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_config_full_size_f32(gpu_ctx, oracle, rtc, name):
+    """configs[2]-[4] at their own sizes on the kernel the bench times: the
+    per-scene build equals the generic kernel bit for bit and meets the f32
+    tolerance against the oracle."""
+    scene, cam, ref, rst = _oracle_frame(oracle, rtc, name)
+    gpu_ctx.upload(scene)
+    img, st = _generic_and_per_scene(gpu_ctx, rtc, cam, 6)
+    _f32_tolerance(name, oracle, img, st, ref, rst)
+
+
+def test_headline_bench_kernel_full_size(gpu_ctx, oracle, rtc):
+    """configs[1] exactly as bench.py runs it (three_sphere_scene 1920x1080,
+    depth 5, f32, the per-scene direct kernel): bit-identical to the generic
+    kernel, >= 99.9 % of pixels within 2/255 of the oracle at the same depth,
+    and 2 W H rays (every pixel meets a wall or the floor)."""
+    scene = scene_fixture("three_sphere_scene")
+    cam = rtc.camera_resize(scene.camera, 1920, 1080)
+    gpu_ctx.upload(scene)
+    img, st = _generic_and_per_scene(gpu_ctx, rtc, cam, 5)
+    ref, rst = oracle.render(scene, cam, 5, threads=ORACLE_THREADS)
+    d = np.abs(oracle.quantize(img).astype(np.int16) - oracle.quantize(ref).astype(np.int16)).max(axis=2)
+    assert float((d <= 2).mean()) >= 0.999
+    assert st["rays"] == rst["rays"] == 2 * 1920 * 1080
 
 
 @pytest.mark.parametrize("name", ["cover", "table"])

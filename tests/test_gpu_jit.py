@@ -5,9 +5,10 @@ world with the shape table as compile-time constants (hipRTC).  Same source,
 same operations, same values: every frame must equal the generic kernel's
 bit for bit, counters included, for every reference scene and for a world
 with every shape and pattern kind.  (Parity with the oracle then carries
-over from tests/test_gpu_parity.py, which runs the generic kernels; the
-full-size tests in tests/test_gpu_fullsize.py run the per-scene kernels,
-their frames being above the 64K-pixel default threshold.)
+over from tests/test_gpu_parity.py, which runs the generic kernels; at the
+bench's own sizes tests/test_gpu_fullsize.py builds the per-scene kernels
+in line (RT_JIT_SYNC), asserts they ran, and checks their frames against
+both the generic kernel and the oracle.)
 """
 import numpy as np
 import pytest
