@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--flags", type=int, default=0, help="RT_FLAG_* diagnostic ablations (profiling only)")
+    ap.add_argument("--gather", choices=["rccl", "peer"], default="rccl",
+                    help="tiled: how rank 0 gets the shards (rtc.h rt_context_set_gather); the other mode is "
+                         "measured too and reported under gather_variants")
     ap.add_argument("--one-shot-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -266,9 +269,13 @@ def main():
     if world > 1 and args.mode == "auto":
         split = measure(resolve(args_for_split(args), True), True, world, rank, local)
         if rank == 0:
+            line["scaling_note"] = ("value: N independent configs[1] frames per step (weak scaling: a throughput "
+                                    "check, linear by construction); the north star's image-tile split is "
+                                    "tile_split (strong scaling: speedup_vs_1gpu over the same frame on one GPU)")
             line["tile_split"] = {k: split[k] for k in (
                 "value", "unit", "ms_per_step", "steps", "scaling", "config", "render_ms_per_shard", "gather_ms",
-                "frame_ms", "single_gpu_ms_per_step", "speedup_vs_1gpu", "single_gpu_value", "roofline",
+                "frame_ms", "gather", "gather_variants", "single_gpu_ms_per_step", "speedup_vs_1gpu",
+                "strong_scaling_efficiency", "single_gpu_value", "roofline",
                 "first_frame_ms") if k in split}
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -307,6 +314,7 @@ def measure(args, tiled, world, rank, local):
         uid = rdist.share_unique_id(rank) if world > 1 else rtc_amd.comm_unique_id()
         t = time.perf_counter()
         ctx = rtc_amd.Context.rank(local, world, rank, uid)
+        ctx.set_gather(rtc_amd.RT_GATHER_PEER if args.gather == "peer" else rtc_amd.RT_GATHER_RCCL)
         phase["context_ms"] = (time.perf_counter() - t) * 1e3
         t = time.perf_counter()
         ctx.upload(scene if rank == 0 else None)
@@ -403,7 +411,28 @@ def measure(args, tiled, world, rank, local):
         kernel_ms = float(np.median([st["kernel_ms"] for st in sts]))
         extra = {"render_ms_per_shard": kernel_ms,
                  "gather_ms": float(np.median([st["gather_ms"] for st in sts])),
-                 "frame_ms": float(np.median([st["frame_ms"] for st in sts]))}
+                 "frame_ms": float(np.median([st["frame_ms"] for st in sts])), "gather": args.gather}
+        # both ways of assembling the frame on rank 0 (rtc.h RT_GATHER_*): the
+        # line's own, then the other one over the same K steps
+        variants = {args.gather: {"ms_per_step": elapsed * 1e3 / args.steps, "frame_ms": extra["frame_ms"],
+                                  "gather_ms": extra["gather_ms"], "render_ms_per_shard": kernel_ms}}
+        other = "peer" if args.gather == "rccl" else "rccl"
+        ctx.set_gather(rtc_amd.RT_GATHER_PEER if other == "peer" else rtc_amd.RT_GATHER_RCCL)
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t = time.perf_counter()
+        timed()
+        el2, _ = rdist.job_totals(time.perf_counter() - t, rays, "cpu")
+        sts2 = [ctx.render_stats(cam, args.depth, args.precision, args.out, host) for _ in range(5)]
+        variants[other] = {"ms_per_step": el2 * 1e3 / args.steps,
+                           "frame_ms": float(np.median([st["frame_ms"] for st in sts2])),
+                           "gather_ms": float(np.median([st["gather_ms"] for st in sts2])),
+                           "render_ms_per_shard": float(np.median([st["kernel_ms"] for st in sts2]))}
+        ctx.set_gather(rtc_amd.RT_GATHER_PEER if args.gather == "peer" else rtc_amd.RT_GATHER_RCCL)
+        extra["gather_variants"] = variants
         if world > 1:
             dist.barrier()
         if rank == 0:
@@ -422,6 +451,7 @@ def measure(args, tiled, world, rank, local):
                 single_ms = (time.perf_counter() - t1) * 1e3 / args.steps
                 extra["single_gpu_ms_per_step"] = single_ms
                 extra["speedup_vs_1gpu"] = single_ms / (elapsed * 1e3 / args.steps)
+                extra["strong_scaling_efficiency"] = extra["speedup_vs_1gpu"] / world
                 # the same workload's throughput on one GPU, in the line's unit: the
                 # denominator for this line's scaling (the default N=1 line is
                 # configs[1], three_sphere at 1080p, a different workload)

@@ -338,6 +338,45 @@ int rt_context_set_jit(rt_context* ctx, int mode);
 int rt_jit_status(rt_context* ctx, int* used_last_launch, double* compile_ms, char* log, size_t log_len);
 int rt_jit_wait(rt_context* ctx, double timeout_ms, int* pending);
 
+/* Peer canvas: a frame assembled in place instead of gathered (SURVEY.md
+ * §8e; the north star's "gather of framebuffer strips over xGMI" done as the
+ * shards' own stores into rank 0's image).  The owner creates a device canvas
+ * (an image of `bytes` plus n_flags completion flags and one release flag)
+ * and shares its IPC handle; other processes map it with rt_canvas_open.
+ * rt_render_to_canvas renders shard options.shard_index of
+ * options.shard_count straight into the canvas at its pixels' IMAGE rows,
+ * then raises that shard's flag to `seq`; before rendering it waits (on the
+ * device) until the owner has released frame seq - 1, so a shard never
+ * overwrites a frame still being read.  rt_canvas_wait makes the owner's
+ * stream wait until every flag has reached `seq`; rt_canvas_release marks
+ * frame `seq` consumed (stream-ordered after its readers).  `seq` starts at 1
+ * and grows by one per frame; the flags start at 0.  The waits are bounded:
+ * after timeout_ms a wait ends and RT_ERR_POOL ("peer canvas") is reported
+ * at the context's next synchronous call.  Asynchronous on `hip_stream`
+ * except create / open / close, which synchronize. */
+#define RT_IPC_HANDLE_BYTES 64
+int rt_canvas_create(rt_context* ctx, uint64_t bytes, uint32_t n_flags, void** canvas,
+                     uint8_t handle[RT_IPC_HANDLE_BYTES]);
+int rt_canvas_open(rt_context* ctx, const uint8_t handle[RT_IPC_HANDLE_BYTES], uint64_t bytes, uint32_t n_flags,
+                   void** canvas);
+int rt_canvas_close(rt_context* ctx, void* canvas);
+int rt_render_to_canvas(rt_context* ctx, const rt_camera_desc* camera, const rt_render_options* options,
+                        void* canvas, uint64_t seq, double timeout_ms, void* hip_stream);
+int rt_canvas_wait(rt_context* ctx, void* canvas, uint64_t seq, double timeout_ms, void* hip_stream);
+int rt_canvas_release(rt_context* ctx, void* canvas, uint64_t seq, void* hip_stream);
+/* The canvas image (its first `bytes`) into a host buffer, after everything
+ * submitted to this context's device (synchronous). */
+int rt_canvas_read(rt_context* ctx, void* canvas, void* out_host, uint64_t bytes);
+
+/* How a multi-GPU context brings the shards to rank 0: RT_GATHER_RCCL (the
+ * default) renders strips and ncclGathers + de-interleaves them;
+ * RT_GATHER_PEER renders every shard into one peer canvas on rank 0 (IPC
+ * handle broadcast over RCCL once; peer access within one process) and
+ * copies the finished image to the caller's buffer.  Collective: every rank
+ * sets the same mode. */
+enum { RT_GATHER_RCCL = 0, RT_GATHER_PEER = 1 };
+int rt_context_set_gather(rt_context* ctx, int mode);
+
 /* Cumulative device counters since context creation (after a sync). */
 int rt_read_counters(rt_context* ctx, rt_stats* totals);
 

@@ -24,7 +24,7 @@
 static int usage() {
     std::fprintf(stderr,
                  "usage: rtc <SCENE.yaml> <OUT.png|OUT.ppm> [-r serial|parallel|gpu] [-q] [--width W] [--height H]\n"
-                 "           [--depth D] [--precision f32|f64] [--device N] [--gpus N] [--ppm-binary]\n");
+                 "           [--depth D] [--precision f32|f64] [--device N] [--gpus N] [--ppm-binary] [--timings]\n");
     return 2;
 }
 
@@ -32,7 +32,7 @@ int main(int argc, char** argv) {
     if (argc < 3) return usage();
     const char* scene_path = argv[1];
     const char* out_path = argv[2];
-    bool quiet = false, ppm_binary = false;
+    bool quiet = false, ppm_binary = false, timings = false;
     uint32_t width = 0, height = 0, depth = RT_DEFAULT_MAX_DEPTH, precision = RT_PRECISION_F32;
     int device = 0, gpus = 1;
     for (int i = 3; i < argc; ++i) {
@@ -40,6 +40,7 @@ int main(int argc, char** argv) {
         auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : nullptr; };
         if (a == "-q" || a == "--quiet") quiet = true;
         else if (a == "--ppm-binary") ppm_binary = true;
+        else if (a == "--timings") timings = true;
         else if (a == "-r" || a == "--rendering-mode") {
             const char* v = next();
             if (!v || (std::strcmp(v, "serial") && std::strcmp(v, "parallel") && std::strcmp(v, "gpu"))) return usage();
@@ -56,6 +57,9 @@ int main(int argc, char** argv) {
         } else return usage();
     }
     if (!quiet) std::printf("Rendering image using scene at %s\n", scene_path);
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+    const auto t_load = clk::now();
     rt_scene* scene = nullptr;
     if (rt_scene_load_yaml(scene_path, &scene) != RT_OK) {
         std::fprintf(stderr, "error: %s\n", rt_last_error());
@@ -65,10 +69,14 @@ int main(int argc, char** argv) {
     rt_scene_view_get(scene, &v);
     rt_camera_desc cam = v.camera;
     if (width || height) rt_camera_resize(&cam, width ? width : cam.width, height ? height : cam.height);
+    const double load_ms = ms_since(t_load);
+    const auto t_ctx = clk::now();
     rt_context* ctx = nullptr;
     std::vector<int> devices;
     for (int g = 0; g < gpus; ++g) devices.push_back(device + g);
     const int created = gpus > 1 ? rt_context_create_multi(devices.data(), gpus, &ctx) : rt_context_create(device, &ctx);
+    const double ctx_ms = ms_since(t_ctx);
+    const auto t_up = clk::now();
     if (created != RT_OK ||
         rt_scene_upload(ctx, v.shapes, v.n_shapes, v.materials, v.n_materials, v.patterns, v.n_patterns, v.lights,
                         v.n_lights) != RT_OK) {
@@ -78,6 +86,7 @@ int main(int argc, char** argv) {
     // One frame: the default per-scene policy (RT_JIT_AUTO) starts a hipRTC
     // build only at a world's second large frame, so this render never
     // compiles.
+    const double upload_ms = ms_since(t_up);
     rt_render_options o = {depth, precision, RT_OUT_U8, 0, 1, 0};
     std::vector<uint8_t> img((size_t)cam.width * cam.height * 3);
     rt_stats st;
@@ -87,6 +96,9 @@ int main(int argc, char** argv) {
         return 1;
     }
     double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (timings)  // one-shot cost by phase: the reference times the render call only
+        std::printf("timings: load_ms=%.3f context_ms=%.3f upload_ms=%.3f render_ms=%.3f kernel_ms=%.3f\n", load_ms,
+                    ctx_ms, upload_ms, s * 1e3, st.kernel_ms);
     if (!quiet) {
         std::printf("Image rendered in: %.3fs\n", s);
         std::printf("kernel %.3f ms on %u GPU(s)\n", st.kernel_ms, st.n_shards ? st.n_shards : 1u);

@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -82,6 +83,7 @@ struct rt_context {
     rtc::DeviceWorld<float> w32;
     rtc::DeviceWorld<double> w64;
     rtc::FlopScene flops;  // per-kind shape counts for the algorithmic FLOP model
+    double bright_hit = 1.0, bright_w = 0.0;  // brightness bound of the world (acc_shift_f32)
     // Defaults from A/B on MI355X (scripts/ab_sched.sh, scripts/stamps2.sh):
     // uniform-cost direct tiles -> static stride; high-variance pool tiles ->
     // per-XCD atomic queues; per-lane stores beat LDS-staged ones (the
@@ -93,7 +95,6 @@ struct rt_context {
     bool kind_variants = true;  // RTC_KIND_VARIANTS=0: always the all-kinds kernels
     size_t occ_lds[8] = {};     // occupancy cache: {direct,pool} x {f32,f64} x {global,LDS world}
     int occ_blocks[8] = {};
-    uint32_t direct_grid = 0;    // RTC_DIRECT_GRID: persistent grid size of the direct kernel (0 = resident)
     uint32_t pool_lds_rays = 0;  // RTC_POOL_LDS_RAYS: LDS-resident pool slots (0 = sized for occupancy)
     void* d_spill = nullptr;     // ray-pool overflow regions, one per resident workgroup
     // Heaviest-first tile order for repeated pool launches of the same frame
@@ -107,8 +108,7 @@ struct rt_context {
     bool order_valid = false;
     bool order_built = false;     // d_tile_order holds an order for order_geometry
     // First launch of a frame geometry (no recorded costs): tiles handed out
-    // centre-out instead of in raster order (RTC_COLD_ORDER=center|raster).
-    bool cold_center = true;
+    // centre-out instead of in raster order (full frames; shards keep raster).
     uint32_t* d_cold_order = nullptr;  // centre-out order + item count, for cold_w x cold_h
     uint32_t cold_w = 0, cold_h = 0;
     // Tiles costing more than split_factor x the mean workgroup load are
@@ -127,26 +127,13 @@ struct rt_context {
     uint32_t split_max = 3;
     // Items (tiles or parts) costing more than urgent_factor x the mean
     // workgroup load run at raised wave priority, graded 1/2/3 above 1x/2x/4x
-    // that cost (RTC_URGENT, 0 = none; RTC_URGENT_GRADED=0: priority 3 for
-    // all of them).  Same-box sweep, kernel ms, none / flat 0.25 / flat 0.125 /
+    // that cost (RTC_URGENT, 0 = none; one level for all measured no better).  Same-box sweep, kernel ms, none / flat 0.25 / flat 0.125 /
     // graded 0.125: reflect_refract 0.367 / 0.310 / 0.306 / 0.310, cylinders
     // 0.124 / 0.117 / 0.117 / 0.117, cover 4K 1.014 / 1.023 / 1.011 / 1.011,
     // table 4K, refraction, metal within 1 %; slowest of 8 shards at 4K: cover
     // 0.215 / 0.201 / 0.215 / 0.201, table 0.229 / 0.266 / 0.230 / 0.231.
     double urgent_factor = 0.125;
-    bool urgent_graded = true;
-    // RTC_COLD_PROBE=wr,wt[,split]: the first launch of a frame geometry orders its tiles by estimated
-    // costs (probe_tiles: per sampled primary hit 1 + wr x reflective + wt x
-    // transparent), split by them if split is set.
-    // Off by default: same-box cold kernel ms, centre-out / probe (8,24):
-    // reflect_refract 0.455 / 0.51, refraction 0.42 / 0.49, cover 4K 1.17 /
-    // 1.20, table 4K 1.27 / 1.32, metal 0.090 / 0.112, cylinders 0.23 / 0.17
-    // (profiles/r03_cold_probe_sweep.txt).
-    bool cold_probe = false;
-    float probe_wr = 8.0f, probe_wt = 24.0f;
-    bool probe_split = false;
     int order_builds = 0;        // order_tiles runs for the current signature so far
-    int order_max_builds = 8;    // RTC_ORDER_BUILDS: runs per signature before the order is frozen
     uint64_t scene_gen = 0;      // bumped by every rt_scene_upload
     uint32_t duplicate_shapes = 0;  // shapes value-equal to an earlier one (one identity class)
     std::vector<int32_t> world_slot;  // world index -> slot | kind << 24 of the uploaded table
@@ -193,6 +180,20 @@ struct rt_context {
     void* d_gathered = nullptr;      // rank 0: every strip, shard-major
     size_t gathered_bytes = 0;
     hipEvent_t ev_render0 = nullptr, ev_render1 = nullptr, ev_gather1 = nullptr;  // frame timing
+    // Peer canvases this context created or mapped (rt_canvas_*): image
+    // bytes and flag count per base pointer.
+    struct Canvas {
+        uint64_t bytes = 0;
+        uint32_t n_flags = 0;
+        bool owned = false;  // created here (hipFree) or mapped (hipIpcCloseMemHandle / peer pointer)
+    };
+    std::map<void*, Canvas> canvases;
+    // RT_GATHER_PEER groups: the shared canvas (rank 0's allocation; mapped or
+    // peer-accessed on the others) and the frame sequence number.
+    int gather_mode = RT_GATHER_RCCL;
+    void* group_canvas = nullptr;
+    uint64_t group_canvas_bytes = 0;
+    uint64_t canvas_seq = 0;
 };
 
 namespace rtc {
@@ -216,10 +217,20 @@ int validate_scene(const rt_shape_desc* shapes, uint32_t ns, const rt_material_d
 // Flatten and upload the world tables to this device (no validation, no sync).
 int build_scene(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats, uint32_t nm,
                 const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights, uint32_t nl);
+void scene_brightness(const rt_material_desc* mats, uint32_t nm, const rt_pattern_desc* pats, uint32_t np,
+                      const rt_light_desc* lights, uint32_t nl, double* bright_hit, double* bright_w);
 // One frame (or shard strip) of this device into `out_device` on `stream`.
 int capture_jit_table(rt_context* ctx);  // the f32 table of the uploaded world, for rtc_jit.cpp
 int launch_frame(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, uint32_t shard_index,
-                 uint32_t shard_count, void* out_device, hipStream_t stream);
+                 uint32_t shard_count, void* out_device, hipStream_t stream, bool image_rows = false);
+// Peer canvas internals (rtc_host.cpp): flags of a canvas, and the kernels.
+unsigned long long* canvas_flags(void* canvas, uint64_t image_bytes);  // n_flags ready flags, then release
+int canvas_create(rt_context* ctx, uint64_t bytes, uint32_t n_flags, void** canvas);
+int canvas_close(rt_context* ctx, void* canvas);
+hipError_t launch_canvas_signal(unsigned long long* flag, unsigned long long seq, hipStream_t stream);
+hipError_t launch_canvas_wait(const unsigned long long* flags, uint32_t n, unsigned long long seq,
+                              unsigned long long timeout_ticks, int32_t* err, hipStream_t stream);
+unsigned long long timeout_ticks(double timeout_ms);
 // rtc_jit.cpp: the per-scene kernel of this context's world for a launch of
 // `static_blocks` workgroups per CU, or null (use the generic kernel)
 constexpr uint32_t kJitMinTiles = 256;  // 64K pixels

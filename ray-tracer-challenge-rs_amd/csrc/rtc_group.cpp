@@ -59,6 +59,7 @@ struct SceneHeader {
     int32_t any_secondary;
     uint32_t duplicates;
     double flops_per_ray;
+    double bright_hit, bright_w;  // acc_shift_f32's bound
 };
 
 template <typename R>
@@ -121,8 +122,12 @@ size_t pixel_bytes(const rt_render_options* o) {
 // stream (rank 0's on `root_stream`), RCCL gathers the strips onto rank 0,
 // rank 0 de-interleaves them into `image` (rank 0's device).  With `timed`,
 // events bracket each member's render and rank 0's gather + assemble.
+int render_shards_peer(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, void* image,
+                       hipStream_t root_stream, bool timed);
+
 int render_shards(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, void* image,
                   hipStream_t root_stream, bool timed) {
+    if (ctx->gather_mode == RT_GATHER_PEER) return render_shards_peer(ctx, cam, o, image, root_stream, timed);
     const std::vector<rt_context*> ms = members(ctx);
     const uint32_t G = (uint32_t)ctx->n_ranks;
     const uint32_t rows = tile_rows_for(cam->height, G, 0) * RT_TILE_H;  // shard 0 has the most rows
@@ -151,6 +156,111 @@ int render_shards(rt_context* ctx, const rt_camera_desc* cam, const rt_render_op
         RT_HIP(hipSetDevice(m->device));
         RT_HIP(launch_assemble(m->d_gathered, image, cam->width, cam->height, G, rows, (uint32_t)pixel_bytes(o),
                                root_stream));
+        if (timed) RT_HIP(hipEventRecord(m->ev_gather1, root_stream));
+    }
+    return RT_OK;
+}
+
+// RT_GATHER_PEER: the group's canvas on rank 0, big enough for `bytes` of
+// image (every rank asks for the same size: collective).  One process per
+// GPU: rank 0 creates it and RCCL-broadcasts its IPC handle, the others map
+// it.  One process with several GPUs: the other members write through peer
+// access to rank 0's pointer.
+int ensure_group_canvas(rt_context* ctx, uint64_t bytes) {
+    const std::vector<rt_context*> ms = members(ctx);
+    if (ctx->group_canvas && ctx->group_canvas_bytes >= bytes) return RT_OK;
+    const uint32_t G = (uint32_t)ctx->n_ranks;
+    const bool remote = (int)ms.size() < ctx->n_ranks;  // ranks in other processes
+    int rc;
+    for (rt_context* m : ms) {  // drop the old canvas (rank 0's allocation, a mapping, or a peer pointer)
+        if (m->group_canvas && m->canvases.count(m->group_canvas) && (rc = canvas_close(m, m->group_canvas))) return rc;
+        m->group_canvas = nullptr;
+        m->group_canvas_bytes = 0;
+    }
+    void* root = nullptr;
+    for (rt_context* m : ms)
+        if (m->rank == 0) {
+            if ((rc = canvas_create(m, bytes, G, &root))) return rc;
+            m->group_canvas = root;
+            m->group_canvas_bytes = bytes;
+        }
+    if (remote) {  // the IPC handle from rank 0 to every rank, over RCCL
+        hipIpcMemHandle_t h{};
+        if (root) {
+            RT_HIP(hipSetDevice(ctx->device));
+            RT_HIP(hipIpcGetMemHandle(&h, root));
+        }
+        std::vector<void*> d_h(ms.size(), nullptr);
+        for (size_t i = 0; i < ms.size(); ++i) {
+            RT_HIP(hipSetDevice(ms[i]->device));
+            RT_HIP(hipMalloc(&d_h[i], sizeof h));
+            if (ms[i]->rank == 0) RT_HIP(hipMemcpy(d_h[i], &h, sizeof h, hipMemcpyHostToDevice));
+        }
+        RT_NCCL(ncclGroupStart());
+        for (size_t i = 0; i < ms.size(); ++i)
+            RT_NCCL(ncclBroadcast(d_h[i], d_h[i], sizeof h, ncclUint8, 0, ms[i]->comm, ms[i]->stream));
+        RT_NCCL(ncclGroupEnd());
+        for (size_t i = 0; i < ms.size(); ++i) {
+            RT_HIP(hipSetDevice(ms[i]->device));
+            RT_HIP(hipStreamSynchronize(ms[i]->stream));
+            hipIpcMemHandle_t got;
+            RT_HIP(hipMemcpy(&got, d_h[i], sizeof got, hipMemcpyDeviceToHost));
+            (void)hipFree(d_h[i]);
+            if (ms[i]->rank == 0) continue;
+            void* p = nullptr;
+            RT_HIP(hipIpcOpenMemHandle(&p, got, hipIpcMemLazyEnablePeerAccess));
+            ms[i]->canvases[p] = {bytes, G, false};
+            ms[i]->group_canvas = p;
+            ms[i]->group_canvas_bytes = bytes;
+        }
+    } else {  // every rank in this process: peer access to rank 0's device
+        for (rt_context* m : ms) {
+            if (m->rank == 0) continue;
+            RT_HIP(hipSetDevice(m->device));
+            if (m->device != ctx->device) {
+                hipError_t e = hipDeviceEnablePeerAccess(ctx->device, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                    return set_error(RT_ERR_HIP, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+                (void)hipGetLastError();
+            }
+            m->group_canvas = root;
+            m->group_canvas_bytes = bytes;
+        }
+    }
+    return RT_OK;
+}
+
+// RT_GATHER_PEER frame: each member waits until rank 0 has released the
+// previous frame, renders its shard at image rows into the canvas and raises
+// its flag; rank 0 waits for every flag, copies the image out and releases
+// the frame.  No strip, no gather, no de-interleave.
+constexpr double kPeerTimeoutMs = 10000.0;
+int render_shards_peer(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, void* image,
+                       hipStream_t root_stream, bool timed) {
+    const std::vector<rt_context*> ms = members(ctx);
+    const uint32_t G = (uint32_t)ctx->n_ranks;
+    const uint64_t bytes = (uint64_t)cam->width * cam->height * pixel_bytes(o);
+    int rc;
+    if ((rc = ensure_group_canvas(ctx, bytes))) return rc;
+    auto stream_of = [&](rt_context* m) { return m->rank == 0 ? root_stream : m->stream; };
+    for (rt_context* m : ms) {
+        hipStream_t s = stream_of(m);
+        RT_HIP(hipSetDevice(m->device));
+        const uint64_t seq = ++m->canvas_seq;  // every rank renders the same frames: the same number
+        unsigned long long* flags = canvas_flags(m->group_canvas, m->group_canvas_bytes);
+        if (seq > 1) RT_HIP(launch_canvas_wait(flags + G, 1, seq - 1, timeout_ticks(kPeerTimeoutMs), m->d_error, s));
+        if (timed) RT_HIP(hipEventRecord(m->ev_render0, s));
+        if ((rc = launch_frame(m, cam, o, (uint32_t)m->rank, G, m->group_canvas, s, true))) return rc;
+        if (timed) RT_HIP(hipEventRecord(m->ev_render1, s));
+        RT_HIP(launch_canvas_signal(flags + m->rank, seq, s));
+    }
+    for (rt_context* m : ms) {
+        if (m->rank != 0) continue;
+        RT_HIP(hipSetDevice(m->device));
+        unsigned long long* flags = canvas_flags(m->group_canvas, m->group_canvas_bytes);
+        RT_HIP(launch_canvas_wait(flags, G, m->canvas_seq, timeout_ticks(kPeerTimeoutMs), m->d_error, root_stream));
+        if (image) RT_HIP(hipMemcpyAsync(image, m->group_canvas, bytes, hipMemcpyDeviceToDevice, root_stream));
+        RT_HIP(launch_canvas_signal(flags + G, m->canvas_seq, root_stream));
         if (timed) RT_HIP(hipEventRecord(m->ev_gather1, root_stream));
     }
     return RT_OK;
@@ -196,6 +306,8 @@ int group_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns
         root_h.any_secondary = ctx->w32.scene.any_secondary;
         root_h.duplicates = ctx->duplicate_shapes;
         root_h.flops_per_ray = ctx->flops.per_ray;
+        root_h.bright_hit = ctx->bright_hit;
+        root_h.bright_w = ctx->bright_w;
     }
     // 1. the header
     std::vector<SceneHeader*> d_hdr(ms.size(), nullptr);
@@ -261,6 +373,8 @@ int group_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns
         m->flops = FlopScene{};
         m->flops.per_ray = h.flops_per_ray;
         m->flops.n_lights = h.nl;
+        m->bright_hit = h.bright_hit;
+        m->bright_w = h.bright_w;
         m->duplicate_shapes = h.duplicates;
         m->have_scene = true;
         ++m->scene_gen;
@@ -438,6 +552,12 @@ int rt_context_create_rank(int device, int n_ranks, int rank, const uint8_t id[R
         return rc;
     }
     *out = m;
+    return RT_OK;
+}
+
+int rt_context_set_gather(rt_context* ctx, int mode) {
+    if (!ctx || (mode != RT_GATHER_RCCL && mode != RT_GATHER_PEER)) return set_error(RT_ERR_INVALID, "bad arguments");
+    for (rt_context* m : members(ctx)) m->gather_mode = mode;
     return RT_OK;
 }
 

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -41,8 +42,6 @@ hipError_t launch_trace(const LaunchParams<R>& P, bool pool, bool dup, uint32_t 
 }  // namespace sp
 constexpr uint32_t kKindsSp = (1u << RT_SHAPE_SPHERE) | (1u << RT_SHAPE_PLANE);
 
-template <typename R>
-hipError_t launch_probe(const LaunchParams<R>& P, float wr, float wt, hipStream_t stream);
 hipError_t launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, uint32_t* n_items, float split_per_cost,
                               uint32_t max_split_log2, float urgent_per_cost, uint32_t graded, hipStream_t stream);
 template <typename R>
@@ -299,7 +298,22 @@ uint32_t pool_capacity(uint32_t depth, uint32_t batch) { return (uint32_t)kBlock
 
 template <typename R>
 size_t pool_lds_bytes(uint32_t cap) {
-    return 3 * kBlock * sizeof(long long) + (size_t)cap * (7 * sizeof(R) + sizeof(uint32_t));
+    return 3 * kBlock * sizeof(PoolAcc<R>) + (size_t)cap * (7 * sizeof(R) + sizeof(uint32_t));
+}
+
+// Scale of the f32 pool kernel's int32 pixel sums (rtc_internal.hpp
+// PoolAcc): the largest 2^s with the world's brightest possible pixel below
+// 2^30 / 2^s.  A shaded hit adds at most bright_hit (per light, the
+// intensity times the material's colour x (ambient + diffuse) + specular,
+// material.rs:83-114) and a hit's children carry at most bright_w of its
+// weight (reflectiveness + transparency, world.rs:54-66: Schlick's R and
+// 1 - R are in [0, 1]), so a pixel is below bright_hit x sum_{g<=depth} bright_w^g.
+uint32_t acc_shift_f32(double bright_hit, double bright_w, uint32_t depth) {
+    double tree = 0.0, w = 1.0;
+    for (uint32_t g = 0; g <= depth; ++g, w *= bright_w) tree += w;
+    const double bound = std::max(bright_hit * tree, 1e-30);
+    const int s = 30 - (int)std::ceil(std::log2(bound));
+    return (uint32_t)std::min<int>(kAccLog2Max, std::max<int>(kAccLog2Min, s));
 }
 
 constexpr size_t kLdsPerCu = 160 * 1024;
@@ -412,8 +426,6 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
     const bool oversub = !ls.pool && ls.sched == kSchedStatic && sizeof(R) == 4;
     const uint64_t grid_cap = oversub ? resident * 5 / 2 : resident;
     ls.grid = ls.sched != kSchedGrid ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, grid_cap)) : n_tiles;
-    if (!ls.pool && ls.sched == kSchedStatic && ctx->direct_grid > 0)  // RTC_DIRECT_GRID (A/B)
-        ls.grid = std::min<uint32_t>(n_tiles, ctx->direct_grid);
     return RT_OK;
 }
 
@@ -463,28 +475,18 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
     if (!same) ctx->order_builds = 0;
     if (!ctx->order_valid || ctx->order_geometry != geometry) ctx->order_built = false;
     uint32_t* n_items = ctx->d_tile_order + ((size_t)ctx->order_capacity << kMaxSplitLog2);
-    if ((same || moved) && ctx->order_builds < ctx->order_max_builds) {
+    if ((same || moved) && ctx->order_builds < kOrderBuilds) {
         const float split = ctx->split_factor > 0 ? (float)(ctx->split_factor / grid) : 0.0f;
         const float urgent = ctx->urgent_factor > 0 ? (float)(ctx->urgent_factor / grid) : 0.0f;
         RT_HIP(launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, P.n_tiles, n_items, split, ctx->split_max,
-                                  urgent, ctx->urgent_graded, stream));
+                                  urgent, 1u, stream));
         ++ctx->order_builds;
-        ctx->order_built = true;
-    }
-    if (!ctx->order_built && ctx->cold_probe) {
-        // No costs yet: estimate them (probe_tiles) and order by the estimate.
-        P.tile_cost = ctx->d_tile_cost;
-        RT_HIP(launch_probe<R>(P, ctx->probe_wr, ctx->probe_wt, stream));
-        const float split = ctx->split_factor > 0 && ctx->probe_split ? (float)(ctx->split_factor / grid) : 0.0f;
-        const float urgent = ctx->urgent_factor > 0 ? (float)(ctx->urgent_factor / grid) : 0.0f;
-        RT_HIP(launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, P.n_tiles, n_items, split, ctx->split_max,
-                                  urgent, ctx->urgent_graded, stream));
         ctx->order_built = true;
     }
     if (ctx->order_built) {  // built from this frame's costs, or from the previous camera's frame
         P.tile_order = ctx->d_tile_order;
         P.item_count = n_items;
-    } else if (ctx->cold_center && P.shard_count == 1) {
+    } else if (P.shard_count == 1) {
         // No costs yet: tiles nearest the image centre first.  The order
         // depends on the canvas only, so it is built and uploaded once per
         // canvas size into its own buffer (order_tiles reuses d_tile_order).
@@ -531,9 +533,10 @@ int order_after_last(rt_context* ctx, hipStream_t stream) {
 template <typename R>
 int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const double* d_rays, uint64_t n_rays,
            uint32_t depth, uint32_t out_format, uint32_t shard_index, uint32_t shard_count, void* out_device,
-           hipStream_t stream, uint32_t flags = 0) {
+           hipStream_t stream, uint32_t flags = 0, bool image_rows = false) {
     int rc;
     LaunchParams<R> P{};
+    P.image_rows = image_rows ? 1u : 0u;
     P.scene = w.scene;
     if (cam) {
         for (int q = 0; q < 12; ++q) P.cam.inv[q] = (R)cam->inverse[q];
@@ -568,6 +571,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     P.pool_capacity = ls.cap;
     P.pool_lds_capacity = ls.lcap;
     P.pop_batch = ls.batch;
+    P.acc_log2 = acc_shift_f32(ctx->bright_hit, ctx->bright_w, depth);
     if (ls.cap > ls.lcap) {
         const size_t need = (size_t)ls.grid * 8 * (ls.cap - ls.lcap) * sizeof(R);
         if (ctx->spill_bytes < need) {
@@ -755,6 +759,7 @@ std::string device_error_text(int32_t err) {
     add(kErrBoundsSpill, "bounds check: spill region outside the spill buffer");
     add(kErrBoundsTile, "bounds check: work item tile outside the launch");
     add(kErrBoundsOut, "bounds check: output index outside the canvas");
+    add(kErrPeerTimeout, "peer canvas: a shard's flag (or the owner's release) did not arrive within the timeout");
     return m.empty() ? "device error " + std::to_string(err) : m;
 }
 
@@ -835,25 +840,10 @@ int create_device_context(int device_ordinal, rt_context** out) {
     if (const char* e = std::getenv("RTC_KIND_VARIANTS")) ctx->kind_variants = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTC_POOL_LDS_RAYS")) ctx->pool_lds_rays = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("RTC_TILE_ORDER")) ctx->tile_order = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("RTC_COLD_ORDER")) ctx->cold_center = !std::strcmp(e, "center");
     if (const char* e = std::getenv("RTC_SPLIT")) ctx->split_factor = std::atof(e);
     if (const char* e = std::getenv("RTC_SPLIT_MAX"))
         ctx->split_max = (uint32_t)std::min<int>((int)kMaxSplitLog2, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("RTC_URGENT")) ctx->urgent_factor = std::atof(e);
-    if (const char* e = std::getenv("RTC_COLD_PROBE")) {  // 0 = off, or "wr,wt[,split]"
-        ctx->cold_probe = std::strcmp(e, "0") != 0;
-        float wr = 0, wt = 0;
-        int sp = 0;
-        const int n = std::sscanf(e, "%f,%f,%d", &wr, &wt, &sp);
-        if (n >= 2) {
-            ctx->probe_wr = wr;
-            ctx->probe_wt = wt;
-        }
-        if (n >= 3) ctx->probe_split = sp != 0;
-    }
-    if (const char* e = std::getenv("RTC_URGENT_GRADED")) ctx->urgent_graded = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("RTC_ORDER_BUILDS")) ctx->order_max_builds = std::atoi(e);
-    if (const char* e = std::getenv("RTC_DIRECT_GRID")) ctx->direct_grid = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("RTC_JIT"))
         ctx->jit_mode = (e[0] >= '0' && e[0] <= '3' && !e[1]) ? e[0] - '0' : RT_JIT_AUTO;
     RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
@@ -879,6 +869,11 @@ void destroy_device_context(rt_context* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();  // launches on caller streams too
+    for (auto& c : ctx->canvases) {
+        if (c.second.owned) (void)hipFree(c.first);
+        else (void)hipIpcCloseMemHandle(c.first);
+    }
+    ctx->canvases.clear();
     ctx->w32.release();
     ctx->w64.release();
     (void)hipFree(ctx->d_tile_counter);
@@ -925,6 +920,30 @@ int rt_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, c
 
 namespace rtc {
 
+// The brightness bound of acc_shift_f32 for these tables.
+void scene_brightness(const rt_material_desc* mats, uint32_t nm, const rt_pattern_desc* pats, uint32_t np,
+                      const rt_light_desc* lights, uint32_t nl, double* bright_hit, double* bright_w) {
+    double pat = 0.0;  // any pattern colour a material may show (complex sub-patterns included)
+    for (uint32_t i = 0; i < np; ++i)
+        for (int c = 0; c < 3; ++c) pat = std::max({pat, std::fabs(pats[i].color_a[c]), std::fabs(pats[i].color_b[c])});
+    double per_light = 0.0, w = 0.0;
+    for (uint32_t i = 0; i < nm; ++i) {
+        const rt_material_desc& m = mats[i];
+        double c = m.pattern >= 0 ? pat : 0.0;
+        for (int k = 0; k < 3; ++k) c = std::max(c, std::fabs(m.color[k]));
+        per_light = std::max(per_light, c * (std::fabs(m.ambient) + std::fabs(m.diffuse)) + std::fabs(m.specular));
+        w = std::max(w, std::fabs(m.reflectiveness) + std::fabs(m.transparency));
+    }
+    double hit = 0.0;
+    for (uint32_t l = 0; l < nl; ++l) {
+        double in = 0.0;
+        for (int k = 0; k < 3; ++k) in = std::max(in, std::fabs(lights[l].intensity[k]));
+        hit += in * per_light;
+    }
+    *bright_hit = std::isfinite(hit) ? hit : 1e300;
+    *bright_w = std::isfinite(w) ? w : 1e300;
+}
+
 int build_scene(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats, uint32_t nm,
                 const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights, uint32_t nl) {
     int rc;
@@ -940,6 +959,7 @@ int build_scene(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const
         ctx->flops.per_ray += shape_test_flops(d.kind, d.closed != 0);
     }
     ctx->flops.n_lights = nl;
+    scene_brightness(mats, nm, pats, np, lights, nl, &ctx->bright_hit, &ctx->bright_w);
     ctx->have_scene = true;
     ++ctx->scene_gen;  // invalidates the recorded tile costs
     return RT_OK;
@@ -976,14 +996,146 @@ int capture_jit_table(rt_context* ctx) {
 }
 
 int launch_frame(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, uint32_t shard_index,
-                 uint32_t shard_count, void* out_device, hipStream_t s) {
+                 uint32_t shard_count, void* out_device, hipStream_t s, bool image_rows) {
     RT_HIP(hipSetDevice(ctx->device));
     if (o->precision == RT_PRECISION_F32)
         return launch<float>(ctx, ctx->w32, cam, nullptr, 0, o->max_depth, o->out_format, shard_index, shard_count,
-                             out_device, s, o->flags);
+                             out_device, s, o->flags, image_rows);
     return launch<double>(ctx, ctx->w64, cam, nullptr, 0, o->max_depth, o->out_format, shard_index, shard_count,
-                          out_device, s, o->flags);
+                          out_device, s, o->flags, image_rows);
 }
+
+// ------------------------------------------------------------ peer canvas
+unsigned long long* canvas_flags(void* canvas, uint64_t image_bytes) {
+    return reinterpret_cast<unsigned long long*>(static_cast<unsigned char*>(canvas) + canvas_flag_offset(image_bytes));
+}
+
+unsigned long long timeout_ticks(double timeout_ms) {  // s_memrealtime runs at 100 MHz
+    return timeout_ms < 0 ? ~0ull : (unsigned long long)(timeout_ms * 1e5);
+}
+
+int canvas_create(rt_context* ctx, uint64_t bytes, uint32_t n_flags, void** canvas) {
+    RT_HIP(hipSetDevice(ctx->device));
+    const size_t flag_bytes = ((size_t)n_flags + 1) * sizeof(unsigned long long);  // ready flags + release
+    void* p = nullptr;
+    RT_HIP(hipMalloc(&p, canvas_flag_offset(bytes) + flag_bytes));
+    if (hipError_t e = hipMemset(canvas_flags(p, bytes), 0, flag_bytes); e != hipSuccess) {
+        (void)hipFree(p);
+        return set_error(RT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e));
+    }
+    ctx->canvases[p] = {bytes, n_flags, true};
+    *canvas = p;
+    return RT_OK;
+}
+
+int canvas_close(rt_context* ctx, void* canvas) {
+    auto it = ctx->canvases.find(canvas);
+    if (it == ctx->canvases.end()) return set_error(RT_ERR_INVALID, "not a canvas of this context");
+    RT_HIP(hipSetDevice(ctx->device));
+    RT_HIP(hipDeviceSynchronize());
+    const bool owned = it->second.owned;
+    ctx->canvases.erase(it);
+    if (owned) RT_HIP(hipFree(canvas));
+    else RT_HIP(hipIpcCloseMemHandle(canvas));
+    return RT_OK;
+}
+
+}  // namespace rtc
+
+extern "C" {
+
+int rt_canvas_create(rt_context* ctx, uint64_t bytes, uint32_t n_flags, void** canvas,
+                     uint8_t handle[RT_IPC_HANDLE_BYTES]) {
+    static_assert(sizeof(hipIpcMemHandle_t) == RT_IPC_HANDLE_BYTES, "RT_IPC_HANDLE_BYTES must match hipIpcMemHandle_t");
+    if (!ctx || !canvas || n_flags == 0 || bytes == 0) return set_error(RT_ERR_INVALID, "rt_canvas_create: bad arguments");
+    int rc = canvas_create(ctx, bytes, n_flags, canvas);
+    if (rc || !handle) return rc;
+    hipIpcMemHandle_t h;
+    if (hipError_t e = hipIpcGetMemHandle(&h, *canvas); e != hipSuccess) {
+        (void)canvas_close(ctx, *canvas);
+        *canvas = nullptr;
+        return set_error(RT_ERR_HIP, std::string("hipIpcGetMemHandle: ") + hipGetErrorString(e));
+    }
+    std::memcpy(handle, &h, sizeof h);
+    return RT_OK;
+}
+
+int rt_canvas_open(rt_context* ctx, const uint8_t handle[RT_IPC_HANDLE_BYTES], uint64_t bytes, uint32_t n_flags,
+                   void** canvas) {
+    if (!ctx || !handle || !canvas || n_flags == 0 || bytes == 0)
+        return set_error(RT_ERR_INVALID, "rt_canvas_open: bad arguments");
+    RT_HIP(hipSetDevice(ctx->device));
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle, sizeof h);
+    void* p = nullptr;
+    RT_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+    ctx->canvases[p] = {bytes, n_flags, false};
+    *canvas = p;
+    return RT_OK;
+}
+
+int rt_canvas_close(rt_context* ctx, void* canvas) {
+    if (!ctx || !canvas) return set_error(RT_ERR_INVALID, "rt_canvas_close: bad arguments");
+    return canvas_close(ctx, canvas);
+}
+
+int rt_render_to_canvas(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, void* canvas,
+                        uint64_t seq, double timeout_ms, void* hip_stream) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if ((rc = check_options(o))) return rc;
+    if (ctx->comm) return set_error(RT_ERR_INVALID, "rt_render_to_canvas takes a single-GPU context");
+    auto it = ctx->canvases.find(canvas);
+    if (!cam || it == ctx->canvases.end()) return set_error(RT_ERR_INVALID, "null camera or unknown canvas");
+    const rt_context::Canvas& c = it->second;
+    const size_t elem = o->out_format == RT_OUT_U8 ? 1 : (o->precision == RT_PRECISION_F32 ? 4 : 8);
+    if ((uint64_t)cam->width * cam->height * 3 * elem > c.bytes || o->shard_index >= c.n_flags || seq == 0)
+        return set_error(RT_ERR_INVALID, "rt_render_to_canvas: canvas too small, shard without a flag, or seq 0");
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    RT_HIP(hipSetDevice(ctx->device));
+    unsigned long long* flags = canvas_flags(canvas, c.bytes);
+    // the owner has released the previous frame (its readers are done)
+    if (seq > 1) RT_HIP(launch_canvas_wait(flags + c.n_flags, 1, seq - 1, timeout_ticks(timeout_ms), ctx->d_error, s));
+    if (cam->width && cam->height &&
+        (rc = launch_frame(ctx, cam, o, o->shard_index, o->shard_count, canvas, s, true)))
+        return rc;
+    RT_HIP(launch_canvas_signal(flags + o->shard_index, seq, s));
+    return RT_OK;
+}
+
+int rt_canvas_wait(rt_context* ctx, void* canvas, uint64_t seq, double timeout_ms, void* hip_stream) {
+    if (!ctx) return set_error(RT_ERR_INVALID, "null context");
+    auto it = ctx->canvases.find(canvas);
+    if (it == ctx->canvases.end()) return set_error(RT_ERR_INVALID, "unknown canvas");
+    RT_HIP(hipSetDevice(ctx->device));
+    RT_HIP(launch_canvas_wait(canvas_flags(canvas, it->second.bytes), it->second.n_flags, seq, timeout_ticks(timeout_ms),
+                              ctx->d_error, static_cast<hipStream_t>(hip_stream)));
+    return RT_OK;
+}
+
+int rt_canvas_read(rt_context* ctx, void* canvas, void* out_host, uint64_t bytes) {
+    if (!ctx || !out_host) return set_error(RT_ERR_INVALID, "null argument");
+    auto it = ctx->canvases.find(canvas);
+    if (it == ctx->canvases.end() || bytes > it->second.bytes) return set_error(RT_ERR_INVALID, "unknown canvas or size");
+    RT_HIP(hipSetDevice(ctx->device));
+    RT_HIP(hipDeviceSynchronize());
+    RT_HIP(hipMemcpy(out_host, canvas, bytes, hipMemcpyDeviceToHost));
+    return check_pool_error(ctx);
+}
+
+int rt_canvas_release(rt_context* ctx, void* canvas, uint64_t seq, void* hip_stream) {
+    if (!ctx) return set_error(RT_ERR_INVALID, "null context");
+    auto it = ctx->canvases.find(canvas);
+    if (it == ctx->canvases.end()) return set_error(RT_ERR_INVALID, "unknown canvas");
+    RT_HIP(hipSetDevice(ctx->device));
+    RT_HIP(launch_canvas_signal(canvas_flags(canvas, it->second.bytes) + it->second.n_flags, seq,
+                                static_cast<hipStream_t>(hip_stream)));
+    return RT_OK;
+}
+
+}  // extern "C"
+
+namespace rtc {
 
 }  // namespace rtc
 

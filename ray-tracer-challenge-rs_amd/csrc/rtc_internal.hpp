@@ -83,6 +83,9 @@ constexpr uint32_t kItemTileMask = 0xFFFFFu;
 constexpr uint32_t kItemPartShift = 20, kItemSplitShift = 24, kItemPartMask = 15u, kItemSplitMask = 7u;
 constexpr uint32_t kItemPrioShift = 27;
 constexpr uint32_t kMaxSplitLog2 = 4;  // up to 16 items per tile
+// order_tiles runs on launches 2 .. 1 + kOrderBuilds of a frame signature,
+// then the order is reused (rtc_host.cpp plan_tile_order).
+constexpr int kOrderBuilds = 8;
 constexpr uint32_t kNoItem = 0xFFFFFFFFu;  // next_tile: the launch's items are all taken
 
 // A work item, decoded.  Only launches that hand items out through a tile
@@ -123,6 +126,14 @@ constexpr int32_t kErrBoundsSlot = 4;    // pool slot outside [0, cap)
 constexpr int32_t kErrBoundsSpill = 8;   // spill record outside the launch's spill buffer
 constexpr int32_t kErrBoundsTile = 16;   // work item's tile >= n_tiles
 constexpr int32_t kErrBoundsOut = 32;    // output element outside the canvas or strip
+constexpr int32_t kErrPeerTimeout = 64;  // rt_canvas_wait: a shard's flag did not arrive in time
+
+// Peer canvas (rt_canvas_create): the W x H image and, after it at this
+// alignment, one u64 completion flag per shard.
+constexpr uint64_t kCanvasFlagAlign = 256;
+RTC_HD inline uint64_t canvas_flag_offset(uint64_t image_bytes) {
+    return (image_bytes + kCanvasFlagAlign - 1) / kCanvasFlagAlign * kCanvasFlagAlign;
+}
 // Tile scheduling modes (RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic)
 constexpr uint32_t kSchedGrid = 0;     // one workgroup per tile; the dispatcher balances
 constexpr uint32_t kSchedDynamic = 1;  // resident grid, per-XCD atomic tile queues
@@ -136,6 +147,27 @@ constexpr size_t kMaxWorldLds = 16 * 1024;
 // (nondeterministic) order in which waves add to it.
 constexpr double kAccScale = 281474976710656.0;  // 2^48
 constexpr double kAccInvScale = 1.0 / 281474976710656.0;
+// The f32 pool kernel sums in int32 multiples of 2^-acc_log2 instead: half
+// the LDS (3 KB of a workgroup's ~26 KB, given to the ray pool), and the
+// scale is the largest that keeps the world's brightest possible pixel below
+// 2^30 (acc_shift_f32), e.g. 2^-22 for reflect_refract: 2.4e-7 per
+// contribution against an f32 ulp of 1.2e-7 at 1.0.
+template <bool B, typename T, typename F>
+struct Choose {
+    using type = T;
+};
+template <typename T, typename F>
+struct Choose<false, T, F> {
+    using type = F;
+};
+#ifndef RTC_ACC_I64  // (A/B builds: -DRTC_ACC_I64 keeps the f32 sums in int64 too)
+template <typename R>
+using PoolAcc = typename Choose<sizeof(R) == 4, int32_t, long long>::type;
+#else
+template <typename R>
+using PoolAcc = long long;
+#endif
+constexpr uint32_t kAccLog2Min = 8, kAccLog2Max = 28;
 
 // ShapeRec::flags.  Value-equal shapes (shape_identity.hpp) form one identity
 // class; its members are adjacent within their kind's run of the table, the
@@ -238,12 +270,15 @@ struct LaunchParams {
     uint32_t width, height;  // canvas
     uint32_t tiles_x;        // tiles per row
     uint32_t tile_rows;      // tile rows of THIS shard's strip
+    uint32_t image_rows;     // 1: store pixels at their image rows of a whole W x H canvas (peer canvas),
+                             // 0: at their strip rows (the shard's own strip)
     uint32_t shard_index, shard_count;
     uint32_t n_tiles;        // tiles_x * tile_rows (or ray chunks in color_at mode)
     uint32_t max_depth;      // `remaining` of the primary ray
     uint32_t pool_capacity;  // pool kernel: LIFO bound (rays) per workgroup
     uint32_t pool_lds_capacity;  // of which held in LDS; the rest in `spill`
     uint32_t pop_batch;      // pool kernel: rays popped per iteration (<= kBlock)
+    uint32_t acc_log2;       // f32 pool kernel: pixel sums in int32 multiples of 2^-acc_log2
     uint32_t persistent;     // kSched*: tile scheduling of this launch
     uint32_t flags;          // RT_FLAG_* diagnostic ablations
     uint32_t world_lds;      // bytes of world tables staged at the start of dynamic LDS (0 = none)

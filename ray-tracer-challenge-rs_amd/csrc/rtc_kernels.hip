@@ -1186,7 +1186,7 @@ __device__ inline bool tile_pixel(const LaunchParams<R>& P, uint32_t t, uint32_t
     const uint32_t local_y = lrow * RT_TILE_H + (wave / kPerRow) * kWaveH + lane / RTC_WAVE_W;  // row in the strip
     x = tcol * RT_TILE_W + (wave % kPerRow) * RTC_WAVE_W + lane % RTC_WAVE_W;
     y = shard_image_row(local_y, P.shard_count, P.shard_index);
-    out_idx = (uint64_t)local_y * P.width + x;
+    out_idx = (uint64_t)(P.image_rows ? y : local_y) * P.width + x;
     return x < P.width && y < P.height;
 }
 
@@ -1411,7 +1411,7 @@ __device__ inline void set_wave_prio(uint32_t p) {
 
 // Ray pool: a LIFO of pending rays per workgroup.  Slots [0, lds_cap) live
 // in dynamic LDS after the world tables:
-//   [acc: 3 x kBlock i64][ox oy oz dx dy dz w : lds_cap x R][meta : lds_cap x u32]
+//   [acc: 3 x kBlock PoolAcc<R>][ox oy oz dx dy dz w : lds_cap x R][meta : lds_cap x u32]
 // and slots [lds_cap, cap) in this workgroup's region of P.spill, one 8-word
 // record per entry (AoS: a lane's entry is two dwordx4 stores / loads in f32,
 // where the SoA layout took eight dword instructions per entry).  The LIFO bound cap = P + depth x
@@ -1419,7 +1419,7 @@ __device__ inline void set_wave_prio(uint32_t p) {
 // occupancy (rtc_host.cpp plan_launch), the rare deep excursions spill.
 template <typename R>
 struct Pool {
-    long long* acc;
+    PoolAcc<R>* acc;
     R* lds;    // 8 arrays of lds_cap words: ox oy oz dx dy dz w, then meta (u32)
     R* spill;  // spill_cap records of 8 words (this workgroup's region)
     int lds_cap, spill_cap;
@@ -1554,9 +1554,18 @@ __device__ inline void pool_get(const Pool<R>& pl, int slot, V3<R>& o, V3<R>& d,
     }
 }
 
-__device__ inline void acc_add(long long* acc, uint32_t pix, double v) {
+// One contribution w x surface into pixel `pix`'s fixed-point sum (an LDS
+// atomic: the sum does not depend on the order waves add in).  f64: int64
+// multiples of 2^-48.  f32: int32 multiples of 2^-acc_log2 (the launch's
+// scale, sized to the world's brightness bound by the host, acc_shift_f32):
+// v x 2^s is exact in f32 and rounds to the nearest integer once.
+__device__ inline void acc_add(long long* acc, uint32_t pix, double v, float) {
     const long long q = __double2ll_rn(v * kAccScale);
     if (q) atomicAdd(reinterpret_cast<unsigned long long*>(&acc[pix]), (unsigned long long)q);
+}
+__device__ inline void acc_add(int* acc, uint32_t pix, float v, float scale) {
+    const int q = (int)__builtin_rintf(v * scale);
+    if (q) atomicAdd(&acc[pix], q);
 }
 
 template <typename R, bool kLds, bool kDup>
@@ -1574,8 +1583,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     const uint32_t cap = P.pool_capacity;
     const uint32_t lcap = P.pool_lds_capacity, gcap = cap - lcap;
     Pool<R> pl;
-    pl.acc = reinterpret_cast<long long*>(smem);
-    pl.lds = reinterpret_cast<R*>(smem + 3 * kBlock * sizeof(long long));
+    pl.acc = reinterpret_cast<PoolAcc<R>*>(smem);
+    pl.lds = reinterpret_cast<R*>(smem + 3 * kBlock * sizeof(PoolAcc<R>));
+    const float acc_scale = __builtin_ldexpf(1.0f, (int)P.acc_log2);
     pl.lds_cap = (int)lcap;
     // 8 words per spilled entry; blockIdx.x < grid (persistent launch)
     pl.spill = reinterpret_cast<R*>(P.spill) + spill_word(blockIdx.x, gcap, lcap, lcap);
@@ -1659,9 +1669,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
             if (P.gen_counts) count_generations(P.gen_counts, active, hit, meta >> 8);
 #endif
             if (hit) {
-                acc_add(pl.acc, pix, (double)(sh.surface.x * rw));
-                acc_add(pl.acc + kBlock, pix, (double)(sh.surface.y * rw));
-                acc_add(pl.acc + 2 * kBlock, pix, (double)(sh.surface.z * rw));
+                acc_add(pl.acc, pix, sh.surface.x * rw, acc_scale);
+                acc_add(pl.acc + kBlock, pix, sh.surface.y * rw, acc_scale);
+                acc_add(pl.acc + 2 * kBlock, pix, sh.surface.z * rw, acc_scale);
             }
             __syncthreads();  // pushes complete before the next pop
             if (s_top[cur ^ 1] > (int)cap) {  // overflowed: drop the pool (error already flagged)
@@ -1670,10 +1680,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
                 __syncthreads();
             }
         }
-        const V3<R> c = {(R)((double)pl.acc[tid] * kAccInvScale), (R)((double)pl.acc[kBlock + tid] * kAccInvScale),
-                         (R)((double)pl.acc[2 * kBlock + tid] * kAccInvScale)};
+        const double inv = sizeof(PoolAcc<R>) == 4 ? __builtin_ldexp(1.0, -(int)P.acc_log2) : kAccInvScale;
+        const V3<R> c = {(R)((double)pl.acc[tid] * inv), (R)((double)pl.acc[kBlock + tid] * inv),
+                         (R)((double)pl.acc[2 * kBlock + tid] * inv)};
 #ifdef RTC_BOUNDS_CHECK
-        valid &= in_bounds(!valid || out_idx < (P.rays ? P.n_rays : (uint64_t)P.tile_rows * RT_TILE_H * P.width),
+        valid &= in_bounds(!valid || out_idx < (P.rays ? P.n_rays
+                                                       : (uint64_t)(P.image_rows ? P.height : P.tile_rows * RT_TILE_H) *
+                                                             P.width),
                            P.error_flag, kErrBoundsOut);
 #endif
         if (valid) store_pixel(P, out_idx, c);
@@ -1699,41 +1712,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         __syncthreads();
         if (threadIdx.x == 0) P.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
     }
-}
-
-// Tile-cost estimate for a frame with no recorded costs (its first launch):
-// kProbeSamples primary rays per tile, each charged 1 + wr x [reflective] +
-// wt x [transparent] for the material it hits (in quarter units), summed per
-// tile into P.tile_cost.  order_tiles then hands the tiles out by these
-// estimates, as it does by measured costs on later launches; its split and
-// priority thresholds are relative to the total, so the unit is free.
-constexpr uint32_t kProbeSamples = 16;
-template <typename R>
-__global__ __launch_bounds__(kBlock) void probe_tiles(LaunchParams<R> P, RTC_WORLD_PARAMS(R), float wr, float wt) {
-    const DevScene<R> sc = scene_view<R, false>(P, shapes, materials, patterns, lights, nullptr);
-    const uint32_t t = blockIdx.x * (kBlock / kProbeSamples) + threadIdx.x / kProbeSamples;
-    const uint32_t s = threadIdx.x % kProbeSamples;
-    uint32_t cost = 0;
-    if (t < P.n_tiles) {
-        // sample s: row s % 4 of wave block s / 4, columns spread over the block
-        const uint32_t tid = (s / 4) * 64 + (s % 4) * RTC_WAVE_W + ((s * 7 + 3) % RTC_WAVE_W);
-        uint32_t x, y;
-        uint64_t idx;
-        if (tile_pixel(P, t, tid, x, y, idx)) {
-            V3<R> o, d;
-            camera_ray(P.cam, x, y, o, d);
-            float w = 1.0f;
-            const Hit<R> h = closest_hit(sc, o, d);
-            if (h.slot >= 0) {
-                const MaterialRec<R>& m = sc.lmats[sc.lshapes[h.slot].material];
-                if (m.reflectiveness > (R)0) w += wr;
-                if (m.transparency > (R)0) w += wt;
-            }
-            cost = (uint32_t)(w * 4.0f + 0.5f);
-        }
-    }
-    for (uint32_t off = kProbeSamples / 2; off > 0; off >>= 1) cost += __shfl_xor(cost, off);
-    if (s == 0 && t < P.n_tiles) P.tile_cost[t] = cost;
 }
 
 #ifndef RTC_PRECISION
@@ -1837,6 +1815,41 @@ __global__ __launch_bounds__(kOrderThreads) void order_tiles(uint32_t* __restric
         if (l) cost[i] = 0;
     }
     if (threadIdx.x == 0) *n_items = items;
+}
+
+// Peer canvas completion (rt_render_to_canvas / rt_canvas_wait).  A shard's
+// pixels reach the canvas (local, or another GPU's through an IPC or peer
+// mapping) from its render kernel; this one-thread kernel, stream-ordered
+// after it, publishes flag = seq with a system-scope release (every earlier
+// write of this device visible first), so the canvas owner can consume the
+// frame once every shard's flag holds the frame's sequence number.
+__global__ void canvas_signal(unsigned long long* flag, unsigned long long seq) {
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// Lane i < n polls flag i (system-scope acquire) until it reaches seq, or
+// until timeout_ticks of s_memrealtime (100 MHz) have passed, which raises
+// kErrPeerTimeout: every lane leaves the loop either way, so the kernel
+// always drains.  Stream-ordered before the canvas's consumers.
+__global__ void canvas_wait(const unsigned long long* flags, uint32_t n, unsigned long long seq,
+                            unsigned long long timeout_ticks, int32_t* err) {
+    const uint32_t i = threadIdx.x;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool late = false;
+    for (uint32_t f = i; f < n; f += blockDim.x) {
+        while (__hip_atomic_load(&flags[f], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+                late = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    if (late) atomicOr(err, kErrPeerTimeout);
+    __threadfence_system();
 }
 
 // De-interleave gathered shard strips into one image.
@@ -1978,21 +1991,6 @@ hipError_t launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, uint3
 #endif
 
 template <typename R>
-hipError_t launch_probe(const LaunchParams<R>& P, float wr, float wt, hipStream_t stream) {
-    (void)hipGetLastError();  // see launch_trace
-    const uint32_t grid = (P.n_tiles + kBlock / kProbeSamples - 1) / (kBlock / kProbeSamples);
-    hipLaunchKernelGGL(probe_tiles<R>, dim3(grid), dim3(kBlock), 0, stream, P, P.scene.shapes, P.scene.materials,
-                       P.scene.patterns, P.scene.lights, wr, wt);
-    return hipGetLastError();
-}
-#if RTC_PRECISION != 2
-template hipError_t launch_probe<float>(const LaunchParams<float>&, float, float, hipStream_t);
-#endif
-#if RTC_PRECISION != 1
-template hipError_t launch_probe<double>(const LaunchParams<double>&, float, float, hipStream_t);
-#endif
-
-template <typename R>
 hipError_t launch_debug_shape(const ShapeRec<R>* shapes, int slot, int kind, uint32_t mode, uint32_t world_space,
                               const double* in, uint32_t n, double* out, hipStream_t stream) {
     (void)hipGetLastError();  // see launch_trace
@@ -2007,6 +2005,20 @@ template hipError_t launch_debug_shape<float>(const ShapeRec<float>*, int, int, 
 #if RTC_PRECISION != 1
 template hipError_t launch_debug_shape<double>(const ShapeRec<double>*, int, int, uint32_t, uint32_t, const double*,
                                                uint32_t, double*, hipStream_t);
+#endif
+
+#if RTC_PRECISION != 2
+hipError_t launch_canvas_signal(unsigned long long* flag, unsigned long long seq, hipStream_t stream) {
+    (void)hipGetLastError();  // see launch_trace
+    hipLaunchKernelGGL(canvas_signal, dim3(1), dim3(64), 0, stream, flag, seq);
+    return hipGetLastError();
+}
+hipError_t launch_canvas_wait(const unsigned long long* flags, uint32_t n, unsigned long long seq,
+                              unsigned long long timeout_ticks, int32_t* err, hipStream_t stream) {
+    (void)hipGetLastError();  // see launch_trace
+    hipLaunchKernelGGL(canvas_wait, dim3(1), dim3(64), 0, stream, flags, n, seq, timeout_ticks, err);
+    return hipGetLastError();
+}
 #endif
 
 #if RTC_PRECISION != 2

@@ -40,6 +40,8 @@ RT_OK = 0
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_HIP", -3: "RT_ERR_NO_DEVICE", -4: "RT_ERR_NO_SCENE",
           -5: "RT_ERR_OOM", -6: "RT_ERR_POOL", -7: "RT_ERR_IO", -8: "RT_ERR_COMM"}
 RT_UNIQUE_ID_BYTES = 128
+RT_IPC_HANDLE_BYTES = 64
+RT_GATHER_RCCL, RT_GATHER_PEER = 0, 1
 
 SHAPE_KINDS = {"sphere": 0, "plane": 1, "cube": 2, "cylinder": 3, "cone": 4, "triangle": 5}
 PATTERN_KINDS = {"stripe": 0, "gradient": 1, "ring": 2, "checker": 3, "complex": 4, "test": 5}
@@ -196,6 +198,15 @@ def _load() -> C.CDLL:
         "rt_context_set_jit": (C.c_int, [C.c_void_p, C.c_int]),
         "rt_jit_status": (C.c_int, [C.c_void_p, P(C.c_int), P(C.c_double), C.c_char_p, C.c_size_t]),
         "rt_jit_wait": (C.c_int, [C.c_void_p, C.c_double, P(C.c_int)]),
+        "rt_canvas_create": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, P(C.c_void_p), P(C.c_uint8)]),
+        "rt_canvas_open": (C.c_int, [C.c_void_p, P(C.c_uint8), C.c_uint64, C.c_uint32, P(C.c_void_p)]),
+        "rt_canvas_close": (C.c_int, [C.c_void_p, C.c_void_p]),
+        "rt_render_to_canvas": (C.c_int, [C.c_void_p, P(CameraDesc), P(RenderOptions), C.c_void_p, C.c_uint64,
+                                          C.c_double, C.c_void_p]),
+        "rt_canvas_wait": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_double, C.c_void_p]),
+        "rt_canvas_release": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+        "rt_canvas_read": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+        "rt_context_set_gather": (C.c_int, [C.c_void_p, C.c_int]),
         "rt_debug_intersect": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), C.c_uint64, C.c_uint32, C.c_uint32,
                                          P(C.c_double)]),
         "rt_debug_normal": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), C.c_uint64, C.c_uint32, C.c_uint32,
@@ -219,7 +230,8 @@ EXPORTED_SYMBOLS = (
     "rt_read_generation_counts",
     "rt_debug_stamps", "rt_debug_tile_costs", "rt_debug_item_log", "rt_debug_intersect", "rt_debug_normal", "rt_camera_set_transform",
     "rt_shard_row_map", "rt_context_create_multi", "rt_comm_unique_id", "rt_context_create_rank", "rt_context_group",
-    "rt_context_set_jit", "rt_jit_status", "rt_jit_wait",
+    "rt_context_set_jit", "rt_jit_status", "rt_jit_wait", "rt_canvas_create", "rt_canvas_open", "rt_canvas_close",
+    "rt_render_to_canvas", "rt_canvas_wait", "rt_canvas_release", "rt_canvas_read", "rt_context_set_gather",
     "rt_assemble_shards", "rt_scene_load_yaml", "rt_scene_load_yaml_text", "rt_scene_view_get", "rt_scene_free",
     "rt_camera_make", "rt_camera_resize", "rt_matrix_inverse", "rt_image_write", "rt_image_write_format",
     "rt_canvas_quantize",
@@ -539,6 +551,48 @@ class Context:
         out = np.zeros_like(p)
         _check(_lib.rt_debug_normal(self._h, shape, p.ctypes.data_as(C.POINTER(C.c_double)), p.shape[0],
                                     PRECISIONS[precision], int(world_space), out.ctypes.data_as(C.POINTER(C.c_double))))
+        return out
+
+    def set_gather(self, mode: int) -> None:
+        """Multi-GPU contexts: RT_GATHER_RCCL (strips + ncclGather + de-interleave) or RT_GATHER_PEER (every
+        shard stores into one canvas on rank 0; rtc.h).  Collective."""
+        _check(_lib.rt_context_set_gather(self._h, mode))
+
+    # ------------------------------------------------ peer canvas (rtc.h)
+    def canvas_create(self, nbytes: int, n_flags: int, ipc: bool = True):
+        """(device pointer, IPC handle bytes or None) of a new canvas of `nbytes` + n_flags shard flags."""
+        p = C.c_void_p()
+        h = (C.c_uint8 * RT_IPC_HANDLE_BYTES)()
+        _check(_lib.rt_canvas_create(self._h, nbytes, n_flags, C.byref(p), h if ipc else None))
+        return p.value, (bytes(h) if ipc else None)
+
+    def canvas_open(self, handle: bytes, nbytes: int, n_flags: int) -> int:
+        """Map another process's canvas (its rt_canvas_create handle); returns the device pointer."""
+        h = (C.c_uint8 * RT_IPC_HANDLE_BYTES).from_buffer_copy(handle)
+        p = C.c_void_p()
+        _check(_lib.rt_canvas_open(self._h, h, nbytes, n_flags, C.byref(p)))
+        return p.value
+
+    def canvas_close(self, canvas: int) -> None:
+        _check(_lib.rt_canvas_close(self._h, C.c_void_p(canvas)))
+
+    def render_to_canvas(self, camera: CameraDesc, canvas: int, seq: int, depth: int = RT_DEFAULT_MAX_DEPTH,
+                         precision: str = "f32", out_format: str = "real", shard=(0, 1), stream_ptr: int | None = None,
+                         timeout_ms: float = 10000.0) -> None:
+        opts = self.options(depth, precision, out_format, shard)
+        _check(_lib.rt_render_to_canvas(self._h, C.byref(camera), C.byref(opts), C.c_void_p(canvas), seq,
+                                        float(timeout_ms), C.c_void_p(stream_ptr or 0)))
+
+    def canvas_wait(self, canvas: int, seq: int, timeout_ms: float = 10000.0, stream_ptr: int | None = None) -> None:
+        _check(_lib.rt_canvas_wait(self._h, C.c_void_p(canvas), seq, float(timeout_ms), C.c_void_p(stream_ptr or 0)))
+
+    def canvas_release(self, canvas: int, seq: int, stream_ptr: int | None = None) -> None:
+        _check(_lib.rt_canvas_release(self._h, C.c_void_p(canvas), seq, C.c_void_p(stream_ptr or 0)))
+
+    def canvas_read(self, canvas: int, shape, dtype=np.uint8) -> np.ndarray:
+        """The canvas image as a host array of `shape` (synchronous; raises on a peer-canvas timeout)."""
+        out = np.zeros(shape, dtype=dtype)
+        _check(_lib.rt_canvas_read(self._h, C.c_void_p(canvas), out.ctypes.data_as(C.c_void_p), out.nbytes))
         return out
 
     def counters(self) -> dict:

@@ -40,6 +40,26 @@ for step in "$@"; do
         rc=$?; echo "pool $a rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done
       tail -c 2000 gpurun_out/bench_pool.log; echo ;;
+    ab)  # pool scenes: this tree's build against _lib_acc64 (int64 pixel sums), alternating
+      : > gpurun_out/ab.log
+      for r in 1 2; do
+        for v in _lib _lib_acc64; do
+          for a in "--scene reflect_refract" "--scene cover --width 3840 --height 2160 --steps 300" \
+                   "--scene table --width 3840 --height 2160 --steps 300"; do
+            out=$(RTC_LIBRARY=$L/$v/librtc.so timeout -k 10 200 python bench.py $a --no-cpu-baseline 2>>gpurun_out/ab.log | grep '^{')
+            rc=$?; [ $rc -eq 0 ] || { echo "ab $v $a rc=$rc"; exit 1; }
+            echo "$out" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', d['config']['workload'], 'kernel_ms %.4f' % d['roofline']['kernel_ms'], 'cold', d.get('cold_kernel_ms'), 'jit', d.get('jit_used'))" | tee -a gpurun_out/ab.log
+          done
+        done
+      done ;;
+    jitdump)  # per-scene headers of the bench scenes for scripts/jit_isa.sh
+      mkdir -p gpurun_out/jit
+      for a in "--scene three_sphere_scene" "--scene reflect_refract" "--scene cover --width 3840 --height 2160" \
+               "--scene table --width 3840 --height 2160"; do
+        RTC_JIT_DUMP=gpurun_out/jit RTC_JIT_CACHE=0 timeout -k 10 200 python bench.py $a --steps 20 --no-cpu-baseline \
+          > /dev/null 2>>gpurun_out/jitdump.log || { echo "jitdump $a failed"; exit 1; }
+      done
+      ls gpurun_out/jit ;;
     prof)
       for sc in three_sphere_scene reflect_refract; do
         timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$sc -o run -- \

@@ -32,11 +32,15 @@ def group_ctx(request, rtc):
     ctx.close()
 
 
+@pytest.mark.parametrize("gather", ["rccl", "peer"])
 @pytest.mark.parametrize("name", ["cover", "three_sphere_scene", "reflect_refract"])
-def test_group_frames_equal_single_gpu(gpu_ctx, group_ctx, rtc, name):
+def test_group_frames_equal_single_gpu(gpu_ctx, group_ctx, rtc, name, gather):
+    """Both ways of bringing the shards to rank 0: the RCCL gather of strips and
+    the peer canvas (shards store at image rows, flags, release)."""
     scene = scene_fixture(name)
     cam = rtc.camera_resize(scene.camera, 480, 270)
     assert group_ctx.group() == (1, 0, 1)
+    group_ctx.set_gather(rtc.RT_GATHER_PEER if gather == "peer" else rtc.RT_GATHER_RCCL)
     group_ctx.upload(scene)
     gpu_ctx.upload(scene)
     for precision, fmt in (("f32", "real"), ("f64", "real"), ("f32", "u8")):
