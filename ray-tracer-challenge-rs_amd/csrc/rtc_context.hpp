@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -199,6 +200,17 @@ struct rt_context {
 namespace rtc {
 
 // rtc_host.cpp
+// RTC_TRACE_INIT=1: per-step milliseconds of context creation, upload and
+// the first renders on stderr (the one-shot breakdown).
+class InitTrace {
+public:
+    explicit InitTrace(const char* what);
+    void step(const char* name);
+private:
+    const char* what_;
+    bool on_;
+    std::chrono::steady_clock::time_point t0_, t_;
+};
 int create_device_context(int device, rt_context** out);
 void destroy_device_context(rt_context* ctx);
 int check_ready(rt_context* ctx);

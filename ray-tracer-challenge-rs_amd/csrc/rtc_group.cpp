@@ -176,6 +176,7 @@ int ensure_group_canvas(rt_context* ctx, uint64_t bytes) {
         if (m->group_canvas && m->canvases.count(m->group_canvas) && (rc = canvas_close(m, m->group_canvas))) return rc;
         m->group_canvas = nullptr;
         m->group_canvas_bytes = 0;
+        m->canvas_seq = 0;  // a new canvas's flags start at 0: its first frame is seq 1 on every rank
     }
     void* root = nullptr;
     for (rt_context* m : ms)

@@ -384,10 +384,25 @@ int pool_lds_rays(rt_context* ctx, uint32_t world_lds, uint32_t cap, uint32_t* l
     return RT_OK;
 }
 
+// LDS world of a per-scene kernel that takes the shape records from its
+// instruction stream (rtc_kernels.hip kJitRecords: worlds of <= 255 shapes):
+// the materials and patterns only.
 template <typename R>
-int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t n_tiles, LaunchShape& ls) {
+size_t jit_world_lds_bytes(const DevScene<R>& sc) {
+    return (size_t)sc.n_materials * sizeof(MaterialRec<R>) + (size_t)sc.n_patterns * sizeof(PatternRec<R>);
+}
+#ifndef RTC_JIT_NO_RECORDS  // (A/B builds: -DRTC_JIT_NO_RECORDS keeps the whole world in LDS)
+constexpr int32_t kJitRecordsMaxShapes = 255;
+#else
+constexpr int32_t kJitRecordsMaxShapes = -1;
+#endif
+
+template <typename R>
+int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t n_tiles, LaunchShape& ls,
+                bool jit_records = false) {
     ls.pool = sc.any_secondary && depth > 0;
-    const size_t wb = world_lds_bytes<R>(sc.kind_begin[kNumKinds], sc.n_materials, sc.n_patterns);
+    const size_t wb = jit_records ? std::max<size_t>(16, jit_world_lds_bytes(sc))
+                                  : world_lds_bytes<R>(sc.kind_begin[kNumKinds], sc.n_materials, sc.n_patterns);
     ls.world_lds = (ctx->lds_world && wb <= kMaxWorldLds) ? (uint32_t)wb : 0;
     ls.lds = ls.world_lds;
     ls.cap = ls.lcap = ls.batch = 0;
@@ -568,6 +583,28 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     LaunchShape ls;
     rc = plan_launch<R>(ctx, w.scene, depth, P.n_tiles, ls);
     if (rc) return rc;
+    // value-equal shapes (rt_scene_upload's identity classes) take the pool
+    // kernel whose containers walk aggregates per class
+    const bool dup = ctx->duplicate_shapes > 0;
+    // large f32 frames run the per-scene build of the same kernel (rtc_jit.cpp),
+    // planned with its own (smaller) LDS world when it takes the shape records
+    // from its instruction stream
+    hipFunction_t jf = nullptr;
+    if constexpr (sizeof(R) == 4) {
+        const bool want = cam && !dup &&
+                          !(flags & (RT_FLAG_STAMPS | RT_FLAG_NO_SHADE | RT_FLAG_NO_TRACE | RT_FLAG_GENERATIONS)) &&
+                          (ctx->jit_mode == RT_JIT_SYNC || (ctx->jit_mode >= RT_JIT_AUTO && P.n_tiles >= kJitMinTiles));
+        if (want) {
+            ++ctx->jit_frames;
+            LaunchShape lj = ls;
+            if (ls.world_lds && w.scene.kind_begin[kNumKinds] <= kJitRecordsMaxShapes &&
+                (rc = plan_launch<R>(ctx, w.scene, depth, P.n_tiles, lj, true)))
+                return rc;
+            if ((rc = jit_function(ctx, lj.pool, lj.world_lds != 0, lj.lds, lj.per_cu, &jf))) return rc;
+            if (jf) ls = lj;
+        }
+    }
+    ctx->jit_used = jf != nullptr;
     P.pool_capacity = ls.cap;
     P.pool_lds_capacity = ls.lcap;
     P.pop_batch = ls.batch;
@@ -637,20 +674,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     uint32_t kinds = 0;
     for (int k = 0; k < kNumKinds; ++k)
         if (w.scene.kind_begin[k + 1] > w.scene.kind_begin[k]) kinds |= 1u << k;
-    // value-equal shapes (rt_scene_upload's identity classes) take the pool
-    // kernel whose containers walk aggregates per class
-    const bool dup = ctx->duplicate_shapes > 0;
     const bool sp = sizeof(R) == 4 && ls.pool && ctx->kind_variants && (kinds & ~kKindsSp) == 0 && !dup;
-    // large f32 frames run the per-scene build of the same kernel (rtc_jit.cpp)
-    hipFunction_t jf = nullptr;
-    if constexpr (sizeof(R) == 4) {
-        const bool want = cam && !dup &&
-                          !(flags & (RT_FLAG_STAMPS | RT_FLAG_NO_SHADE | RT_FLAG_NO_TRACE | RT_FLAG_GENERATIONS)) &&
-                          (ctx->jit_mode == RT_JIT_SYNC || (ctx->jit_mode >= RT_JIT_AUTO && P.n_tiles >= kJitMinTiles));
-        if (want) ++ctx->jit_frames;
-        if (want && (rc = jit_function(ctx, ls.pool, ls.world_lds != 0, ls.lds, ls.per_cu, &jf))) return rc;
-    }
-    ctx->jit_used = jf != nullptr;
     if (flags & RT_FLAG_FAIL_LAUNCH) return set_error(RT_ERR_HIP, "launch refused (RT_FLAG_FAIL_LAUNCH)");
     if (jf) {
         const ShapeRec<R>* sh = P.scene.shapes;
@@ -672,6 +696,18 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
                                          " rays in LDS): " + hipGetErrorString(e));
     if (dynamic) ctx->head_set ^= 1;
     return RT_OK;
+}
+
+InitTrace::InitTrace(const char* what) : what_(what), on_(std::getenv("RTC_TRACE_INIT") != nullptr) {
+    t0_ = t_ = std::chrono::steady_clock::now();
+}
+void InitTrace::step(const char* name) {
+    if (!on_) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[rtc init] %s: %s %.3f ms (%.3f ms total)\n", what_, name,
+                 std::chrono::duration<double, std::milli>(now - t_).count(),
+                 std::chrono::duration<double, std::milli>(now - t0_).count());
+    t_ = now;
 }
 
 int check_ready(rt_context* ctx) {
@@ -812,11 +848,16 @@ int create_device_context(int device_ordinal, rt_context** out) {
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
         return set_error(RT_ERR_NO_DEVICE, "no HIP device available (the render path has no CPU fallback)");
     if (device_ordinal < 0 || device_ordinal >= n) return set_error(RT_ERR_INVALID, "device ordinal out of range");
+    // RTC_TRACE_INIT=1: milliseconds of each step of context creation on
+    // stderr (the one-shot render's breakdown)
+    InitTrace tr("context");
     auto ctx = std::make_unique<rt_context>();
     ctx->device = device_ordinal;
     RT_HIP(hipSetDevice(device_ordinal));
+    tr.step("hipSetDevice");
     hipDeviceProp_t prop;
     RT_HIP(hipGetDeviceProperties(&prop, device_ordinal));
+    tr.step("hipGetDeviceProperties");
     ctx->cu_count = prop.multiProcessorCount;
     {  // "gfx950:sramecc+:xnack-" -> "gfx950": the per-scene builds' target
         const std::string a(prop.gcnArchName);
@@ -847,12 +888,16 @@ int create_device_context(int device_ordinal, rt_context** out) {
     if (const char* e = std::getenv("RTC_JIT"))
         ctx->jit_mode = (e[0] >= '0' && e[0] <= '3' && !e[1]) ? e[0] - '0' : RT_JIT_AUTO;
     RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    tr.step("hipStreamCreate");
     RT_HIP(hipEventCreate(&ctx->ev_start));
     RT_HIP(hipEventCreate(&ctx->ev_stop));
     RT_HIP(hipEventCreateWithFlags(&ctx->ev_order, hipEventDisableTiming));
+    tr.step("hipEventCreate x3");
     const size_t qbytes = 2 * (size_t)kTileQueues * kQueueStride * sizeof(unsigned long long);  // two sets
     RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_tile_counter), qbytes));
+    tr.step("hipMalloc");
     RT_HIP(hipMemset(ctx->d_tile_counter, 0, qbytes));
+    tr.step("hipMemset (first)");
     const size_t counter_bytes = (size_t)kCounterShards * kNumCounters * sizeof(unsigned long long);
     RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_counters), counter_bytes));
     RT_HIP(hipMemset(ctx->d_counters, 0, counter_bytes));
@@ -861,6 +906,7 @@ int create_device_context(int device_ordinal, rt_context** out) {
     const size_t gen_bytes = 2 * (size_t)kGenSlots * sizeof(unsigned long long);
     RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_gen_counts), gen_bytes));
     RT_HIP(hipMemset(ctx->d_gen_counts, 0, gen_bytes));
+    tr.step("hipMalloc+hipMemset x3");
     *out = ctx.release();
     return RT_OK;
 }
@@ -1185,8 +1231,11 @@ int rt_render(rt_context* ctx, const rt_camera_desc* cam, const rt_render_option
         if (stats) std::memset(stats, 0, sizeof(*stats));
         return RT_OK;
     }
+    InitTrace tr("rt_render");
     if ((rc = ensure_scratch(ctx, bytes))) return rc;
+    tr.step("scratch");
     if ((rc = ensure_host_counters(ctx))) return rc;
+    tr.step("pinned counters");
     hipStream_t s = ctx->stream;
     // counters before and after, and the error flag, come back in pinned
     // memory on the stream: one host sync for the whole frame
@@ -1198,12 +1247,16 @@ int rt_render(rt_context* ctx, const rt_camera_desc* cam, const rt_render_option
     RT_HIP(hipMemcpyAsync(h_before, ctx->d_counters, cbytes, hipMemcpyDeviceToHost, s));
     if (o->shard_count > 1) RT_HIP(hipMemsetAsync(ctx->d_scratch, 0, bytes, s));  // strip rows past the canvas
     RT_HIP(hipEventRecord(ctx->ev_start, s));
+    tr.step("enqueue before launch");
     if ((rc = launch_frame(ctx, cam, o, o->shard_index, o->shard_count, ctx->d_scratch, s))) return rc;
+    tr.step("launch");
     RT_HIP(hipEventRecord(ctx->ev_stop, s));
     RT_HIP(hipMemcpyAsync(h_after, ctx->d_counters, cbytes, hipMemcpyDeviceToHost, s));
     RT_HIP(hipMemcpyAsync(h_err, ctx->d_error, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     if ((rc = copy_to_host(ctx, out_host, out_bytes))) return rc;
+    tr.step("enqueue copies");
     RT_HIP(hipStreamSynchronize(s));
+    tr.step("synchronize (kernel + copies)");
     float ms = 0.f;
     RT_HIP(hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_stop));
     if (*h_err) {

@@ -427,6 +427,19 @@ __device__ inline void jit_each(F&& f) {
 }
 #endif
 
+// Per-scene builds of worlds of at most 255 shapes take every value of the
+// hit's shape record from the instruction stream: the hit's slot rides in
+// the closest-hit key next to its world index, and its normal, material and
+// pattern-space point come from one branch per slot present among the
+// wave's hits, where the record is constants (jit_record_each).  Their LDS
+// then holds only the materials and patterns (rtc_host.cpp
+// jit_world_lds_bytes), which leaves more of it to the ray pool.
+#if defined(RTC_JIT) && !defined(RTC_JIT_NO_RECORDS)
+constexpr bool kJitRecords = jit::kBegin[kNumKinds] <= 255;  // rtc_host.cpp kJitRecordsMaxShapes
+#else
+constexpr bool kJitRecords = false;
+#endif
+
 // Visit every shape of kind K (wave-uniform loop, scalar loads).
 template <typename R, int K, typename F>
 __device__ inline void for_kind(const DevScene<R>& sc, F&& f) {
@@ -584,6 +597,13 @@ struct Nearest {
     __device__ inline Hit<R> hit(const DevScene<R>& sc) const {
         const int hw = kKeys ? (int)(uint32_t)key : w;
         Hit<R> h{t, -1, hw, -1};
+        if constexpr (kJitRecords && kKeys) {  // key = world << 8 | slot (closest_hit); kind unused
+            if (hw != __INT_MAX__) {
+                h.world = hw >> 8;
+                h.slot = hw & 0xFF;
+            }
+            return h;
+        }
         if (hw != __INT_MAX__) {
             const uint32_t ws = (uint32_t)sc.lworld_slot[hw];
             h.slot = (int)(ws & 0xFFFFFFu);
@@ -607,7 +627,9 @@ __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
         if (!wave_may_hit<R, K>(s, o, d, dd)) return;
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
-        const int w = s.world_index;
+        // (per-scene records: the slot rides below the world index; world
+        // indices are distinct, so the order is the world order)
+        const int w = kJitRecords && sizeof(R) == 4 ? (s.world_index << 8) | slot : s.world_index;
         entries<R, K, true>(s, lo, ld, [&](R t, bool v) { best.offer(t, v, w); });
     });
     return best.hit(sc);
@@ -640,7 +662,7 @@ struct Blocker {
 // is_in_shadow (world.rs:98-112): any casting shape with 0 <= t < distance.
 template <typename R>
 __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) {
-#ifdef RTC_ABLATE_SHADOW  // diagnostic builds only (scripts/gpu_r3ai.sh): time without shadow rays
+#ifdef RTC_ABLATE_SHADOW  // diagnostic builds only (scripts/build_variant.sh -DRTC_ABLATE_...): time without shadow rays
     return false;
 #endif
     Blocker<R> b;
@@ -671,11 +693,11 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) 
 // Same-box A/B, per-class walk in every world vs this split: reflect_refract
 // +3.5%, refraction +2.2% kernel time.
 template <typename R, bool kDup>
-__device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> d, const Hit<R>& h, R& n1,
-                                          R& n2) {
-#ifdef RTC_ABLATE_WALK  // diagnostic builds only (scripts/gpu_r3ai.sh): time without the walk
+__device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> d, const Hit<R>& h, int hit_mat,
+                                          R& n1, R& n2) {
+#ifdef RTC_ABLATE_WALK  // diagnostic builds only (scripts/build_variant.sh -DRTC_ABLATE_...): time without the walk
     n1 = (R)1;
-    n2 = sc.lmats[sc.lshapes[h.slot].material].refractive_index;
+    n2 = sc.lmats[hit_mat].refractive_index;
     return;
 #endif
     struct Key {
@@ -762,7 +784,7 @@ __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> 
     if (flags & kHitPresent)  // the hit's class leaves the list
         n2 = (flags & kHaveOther) ? sc.lmats[mat_other].refractive_index : (R)1;
     else              // the hit pushes itself
-        n2 = sc.lmats[sc.lshapes[h.slot].material].refractive_index;
+        n2 = sc.lmats[hit_mat].refractive_index;
 }
 
 // local_normal_at of each shape (object space, not normalized)
@@ -840,6 +862,27 @@ __device__ inline void jit_normal_each(int slot, V3<float> p, V3<float>& w) {
         jit_normal_each<I + 1, E>(slot, p, w);
     }
 }
+
+// kJitRecords: the hit's unnormalised world normal and material index, and
+// (jit_object_each) the object-space point of p, from a branch per slot
+template <int I, int E>
+__device__ inline void jit_record_each(int slot, V3<float> p, V3<float>& w, int& mat) {
+    if constexpr (I < E) {
+        if (slot == I) {
+            const ShapeRec<float>& s = jit::kShapes[I];
+            w = xform_normal(s.inv, local_normal(s, jit_kind_of<I>(), xform_point(s.inv, p)));
+            mat = s.material;
+        }
+        jit_record_each<I + 1, E>(slot, p, w, mat);
+    }
+}
+template <int I, int E>
+__device__ inline void jit_object_each(int slot, V3<float> p, V3<float>& obj) {
+    if constexpr (I < E) {
+        if (slot == I) obj = xform_point(jit::kShapes[I].inv, p);
+        jit_object_each<I + 1, E>(slot, p, obj);
+    }
+}
 #endif
 
 template <typename R>
@@ -866,10 +909,10 @@ __device__ inline V3<R> hit_normal(const ShapeRec<R>& s, int slot, int kind, V3<
 #define RTC_PATTERN_KIND(k) (void)0
 #endif
 template <typename R>
-__device__ inline V3<R> pattern_color(const DevScene<R>& sc, int pid, const ShapeRec<R>& s, V3<R> p) {
+__device__ inline V3<R> pattern_color_obj(const DevScene<R>& sc, int pid, V3<R> obj) {  // obj: object space
     using T = Real<R>;
     const PatternRec<R>* pr = &sc.lpats[pid];
-    const V3<R> pp = xform_point(pr->inv, xform_point(s.inv, p));
+    const V3<R> pp = xform_point(pr->inv, obj);
     for (int guard = 0; guard < 16; ++guard) {
         switch (pr->kind) {
             case RT_PATTERN_STRIPE:  // stripe_pattern.rs:24-31
@@ -906,6 +949,10 @@ __device__ inline V3<R> pattern_color(const DevScene<R>& sc, int pid, const Shap
         }
     }
     return {(R)0, (R)0, (R)0};
+}
+template <typename R>
+__device__ inline V3<R> pattern_color(const DevScene<R>& sc, int pid, const ShapeRec<R>& s, V3<R> p) {
+    return pattern_color_obj(sc, pid, xform_point(s.inv, p));
 }
 
 // Per-thread event counters (rt_stats order).
@@ -981,16 +1028,41 @@ __device__ inline void count_events(Counts& k, bool primary, bool hit, const Sha
 template <typename R>
 struct Prepared {
     V3<R> p, n, eye, over, base;
+    int mat;  // the hit's material index
 };
 
 template <typename R>
 __device__ inline const MaterialRec<R>& prepare_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, const Hit<R>& h,
                                                      Prepared<R>& q, bool& patterned) {
+#ifdef RTC_JIT
+    if constexpr (kJitRecords && sizeof(R) == 4) {
+        q.p = along(o, d, h.t);
+        V3<float> w = {0.0f, 0.0f, 0.0f};
+        int mat = 0;
+        jit_record_each<0, jit::kBegin[kNumKinds]>(h.slot, q.p, w, mat);
+        asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(w.z));  // the hardware rsq, as hit_normal (bit for bit)
+        q.n = normalized(w);
+        q.eye = vneg(d);
+        if (dot(q.n, q.eye) < (R)0) q.n = vneg(q.n);
+        q.mat = mat;
+        const MaterialRec<R>& m = sc.lmats[mat];
+        q.over = along(q.p, q.n, Real<R>::surface_offset(q.p.x, q.p.y, q.p.z));
+        q.base = {m.color[0], m.color[1], m.color[2]};
+        patterned = m.pattern >= 0;
+        if (jit::kPatterns && patterned) {
+            V3<float> obj = {0.0f, 0.0f, 0.0f};
+            jit_object_each<0, jit::kBegin[kNumKinds]>(h.slot, q.over, obj);
+            q.base = pattern_color_obj(sc, m.pattern, obj);
+        }
+        return m;
+    }
+#endif
     const ShapeRec<R>& s = sc.lshapes[h.slot];
     q.p = along(o, d, h.t);
     q.n = hit_normal(s, h.slot, h.kind, q.p);
     q.eye = vneg(d);
     if (dot(q.n, q.eye) < (R)0) q.n = vneg(q.n);
+    q.mat = s.material;
     const MaterialRec<R>& m = sc.lmats[s.material];
     q.over = along(q.p, q.n, Real<R>::surface_offset(q.p.x, q.p.y, q.p.z));
     q.base = {m.color[0], m.color[1], m.color[2]};
@@ -1089,7 +1161,7 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
 #endif
         const bool reflective = m.reflectiveness > (R)0, transparent = kTransparent && m.transparency > (R)0;
         R n1 = (R)1, n2 = (R)1;
-        if (kTransparent && m.transparency != (R)0) refractive_indices<R, kDup>(sc, o, d, h, n1, n2);
+        if (kTransparent && m.transparency != (R)0) refractive_indices<R, kDup>(sc, o, d, h, q.mat, n1, n2);
         // Schlick mixing only when both (world.rs:59-66)
         R fr = (R)1, ft = (R)1;
         if (reflective && transparent) {  // computed_hit.rs:50-68
@@ -1276,7 +1348,21 @@ __device__ inline DevScene<R> scene_view(const LaunchParams<R>& P, const ShapeRe
     sc.materials = materials;
     sc.patterns = patterns;
     sc.lights = lights;
-    if constexpr (kLds) {
+    if constexpr (kLds && kJitRecords && sizeof(R) == 4) {
+        // per-scene records: only [materials][patterns] in LDS (no shapes, no world_slot)
+        auto* lm = reinterpret_cast<MaterialRec<R>*>(smem);
+        auto* lp = reinterpret_cast<PatternRec<R>*>(lm + sc.n_materials);
+        if (stage) {
+            const uint4* s4 = reinterpret_cast<const uint4*>(materials);  // followed by the patterns (DeviceWorld)
+            uint4* d4 = reinterpret_cast<uint4*>(lm);
+            for (uint32_t i = threadIdx.x; i < P.world_lds / 16; i += kBlock) d4[i] = s4[i];
+            __syncthreads();
+        }
+        sc.lshapes = shapes;
+        sc.lmats = lm;
+        sc.lpats = lp;
+        sc.lworld_slot = sc.world_slot;
+    } else if constexpr (kLds) {
         const int ns = sc.kind_begin[kNumKinds];
         auto* ls = reinterpret_cast<ShapeRec<R>*>(smem);
         auto* lm = reinterpret_cast<MaterialRec<R>*>(ls + ns);

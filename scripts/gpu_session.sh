@@ -40,11 +40,11 @@ for step in "$@"; do
         rc=$?; echo "pool $a rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done
       tail -c 2000 gpurun_out/bench_pool.log; echo ;;
-    ab)  # pool scenes: this tree's build against _lib_acc64 (int64 pixel sums), alternating
+    ab)  # this tree's build against the builds in AB_VARIANTS (rtc_amd/_lib_*), alternating, 2 rounds
       : > gpurun_out/ab.log
       for r in 1 2; do
-        for v in _lib _lib_acc64; do
-          for a in "--scene reflect_refract" "--scene cover --width 3840 --height 2160 --steps 300" \
+        for v in _lib ${AB_VARIANTS:-_lib_acc64}; do
+          for a in "--scene three_sphere_scene" "--scene reflect_refract" "--scene cover --width 3840 --height 2160 --steps 300" \
                    "--scene table --width 3840 --height 2160 --steps 300"; do
             out=$(RTC_LIBRARY=$L/$v/librtc.so timeout -k 10 200 python bench.py $a --no-cpu-baseline 2>>gpurun_out/ab.log | grep '^{')
             rc=$?; [ $rc -eq 0 ] || { echo "ab $v $a rc=$rc"; exit 1; }
@@ -60,6 +60,11 @@ for step in "$@"; do
           > /dev/null 2>>gpurun_out/jitdump.log || { echo "jitdump $a failed"; exit 1; }
       done
       ls gpurun_out/jit ;;
+    oneshot)  # where a one-shot render's time goes (RTC_TRACE_INIT steps), torch-free child, twice
+      for i in 1 2; do
+        RTC_TRACE_INIT=1 timeout -k 10 120 python bench.py --one-shot-child > gpurun_out/oneshot_$i.log 2>&1
+        rc=$?; echo "oneshot rc=$rc"; grep -v amdgpu.ids gpurun_out/oneshot_$i.log; [ $rc -eq 0 ] || exit $rc
+      done ;;
     prof)
       for sc in three_sphere_scene reflect_refract; do
         timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$sc -o run -- \
