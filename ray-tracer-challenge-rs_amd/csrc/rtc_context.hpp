@@ -151,6 +151,7 @@ struct rt_context {
     // (default) | RT_JIT_EAGER (rtc.h).
     std::vector<rtc::ShapeRec<float>> jit_shapes;
     std::vector<rtc::LightRec<float>> jit_lights;  // per-scene builds unroll the lights as constants
+    std::vector<rtc::MaterialRec<float>> jit_materials;  // ... and the direct kernel reads materials as constants
     bool jit_patterns = true;                      // some material has a pattern (else pattern code is dropped)
     uint32_t jit_pattern_kinds = ~0u;              // pattern kinds in the world's table (bit per RT_PATTERN_*)
     bool jit_transparent = true;                   // some material is transparent (else no refraction code)

@@ -403,7 +403,9 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
     ls.pool = sc.any_secondary && depth > 0;
     const size_t wb = jit_records ? std::max<size_t>(16, jit_world_lds_bytes(sc))
                                   : world_lds_bytes<R>(sc.kind_begin[kNumKinds], sc.n_materials, sc.n_patterns);
-    ls.world_lds = (ctx->lds_world && wb <= kMaxWorldLds) ? (uint32_t)wb : 0;
+    // (a per-scene direct kernel takes its materials from constants too and
+    // stages no world at all: rtc_kernels.hip kJitConstMaterials)
+    ls.world_lds = (ctx->lds_world && wb <= kMaxWorldLds && !(jit_records && !ls.pool)) ? (uint32_t)wb : 0;
     ls.lds = ls.world_lds;
     ls.cap = ls.lcap = ls.batch = 0;
     ls.sched = ls.pool ? ctx->sched_pool : (ctx->sched_direct == kSchedDynamic ? kSchedStatic : ctx->sched_direct);
@@ -597,7 +599,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
         if (want) {
             ++ctx->jit_frames;
             LaunchShape lj = ls;
-            if (ls.world_lds && w.scene.kind_begin[kNumKinds] <= kJitRecordsMaxShapes &&
+            if (ctx->lds_world && w.scene.kind_begin[kNumKinds] <= kJitRecordsMaxShapes &&
                 (rc = plan_launch<R>(ctx, w.scene, depth, P.n_tiles, lj, true)))
                 return rc;
             if ((rc = jit_function(ctx, lj.pool, lj.world_lds != 0, lj.lds, lj.per_cu, &jf))) return rc;
@@ -1021,6 +1023,7 @@ int capture_jit_table(rt_context* ctx) {
     if (nl) RT_HIP(hipMemcpy(ctx->jit_lights.data(), ctx->w32.lights, nl * sizeof(LightRec<float>), hipMemcpyDeviceToHost));
     std::vector<MaterialRec<float>> mats(nm);
     if (nm) RT_HIP(hipMemcpy(mats.data(), ctx->w32.materials, nm * sizeof(MaterialRec<float>), hipMemcpyDeviceToHost));
+    ctx->jit_materials = mats;
     ctx->jit_patterns = std::any_of(mats.begin(), mats.end(), [](const MaterialRec<float>& m) { return m.pattern >= 0; });
     ctx->jit_transparent =
         std::any_of(mats.begin(), mats.end(), [](const MaterialRec<float>& m) { return m.transparency != 0.0f; });

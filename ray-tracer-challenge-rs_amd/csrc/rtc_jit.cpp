@@ -95,8 +95,8 @@ std::string floats(const float (&a)[N]) {
 // rtc_jit_scene.hpp: the world's f32 shape table, its lights and whether any
 // material has a pattern, as constexpr data.
 std::string scene_header(const std::vector<ShapeRec<float>>& sh, const int32_t begin[kNumKinds + 1],
-                         const std::vector<LightRec<float>>& lights, bool patterns, uint32_t pattern_kinds,
-                         bool transparent) {
+                         const std::vector<LightRec<float>>& lights, const std::vector<MaterialRec<float>>& mats,
+                         bool patterns, uint32_t pattern_kinds, bool transparent) {
     std::string s = "#pragma once\n#include \"rtc_internal.hpp\"\nnamespace rtc {\nnamespace jit {\n";
     s += "constexpr int kBegin[" + std::to_string(kNumKinds + 1) + "] = {";
     for (int k = 0; k <= kNumKinds; ++k) s += (k ? ", " : "") + std::to_string(begin[k]);
@@ -110,6 +110,13 @@ std::string scene_header(const std::vector<ShapeRec<float>>& sh, const int32_t b
     s += "constexpr int kNumLights = " + std::to_string(lights.size()) + ";\n";
     s += "constexpr LightRec<float> kLights[" + std::to_string(lights.size() + 1) + "] = {\n";
     for (const LightRec<float>& l : lights) s += "    {" + floats(l.position) + ", " + floats(l.intensity) + "},\n";
+    s += "    {}};\n";
+    s += "constexpr MaterialRec<float> kMaterials[" + std::to_string(mats.size() + 1) + "] = {\n";
+    for (const MaterialRec<float>& m : mats) {
+        s += "    {" + floats(m.color) + ", " + hexf(m.ambient) + ", " + hexf(m.diffuse) + ", " + hexf(m.specular) + ", " +
+             hexf(m.shininess) + ", " + hexf(m.reflectiveness) + ", " + hexf(m.transparency) + ", " +
+             hexf(m.refractive_index) + ", " + std::to_string(m.pattern) + ", " + std::to_string(m.casts_shadow) + "},\n";
+    }
     s += "    {}};\n";
     s += std::string("constexpr bool kPatterns = ") + (patterns ? "true" : "false") + ";\n";
     s += "constexpr uint32_t kPatternKinds = " + std::to_string(pattern_kinds) + "u;\n";
@@ -378,6 +385,7 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
         uint64_t table = fnv(ctx->jit_begin, sizeof ctx->jit_begin,
                              fnv(ctx->jit_shapes.data(), ctx->jit_shapes.size() * sizeof(ShapeRec<float>)));
         table = fnv(ctx->jit_lights.data(), ctx->jit_lights.size() * sizeof(LightRec<float>), table);
+        table = fnv(ctx->jit_materials.data(), ctx->jit_materials.size() * sizeof(MaterialRec<float>), table);
         const uint32_t traits[3] = {ctx->jit_patterns, ctx->jit_pattern_kinds, ctx->jit_transparent};
         table = fnv(traits, sizeof traits, table);
         // the device's gfx target: each build is compiled for one (make_request),
@@ -401,7 +409,8 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
             ctx->jit_owner[variant] = true;
             uint64_t key = 0;
             const jitfile::Request rq =
-                make_request(scene_header(ctx->jit_shapes, ctx->jit_begin, ctx->jit_lights, ctx->jit_patterns,
+                make_request(scene_header(ctx->jit_shapes, ctx->jit_begin, ctx->jit_lights, ctx->jit_materials,
+                                          ctx->jit_patterns,
                                           ctx->jit_pattern_kinds, ctx->jit_transparent),
                              kernel_name(pool, lds), ctx->arch, &key);
             start_build(b, rq, key, sync);

@@ -439,6 +439,11 @@ constexpr bool kJitRecords = jit::kBegin[kNumKinds] <= 255;  // rtc_host.cpp kJi
 #else
 constexpr bool kJitRecords = false;
 #endif
+#ifdef RTC_JIT
+// The per-scene DIRECT kernel also takes the hit's material from constants
+// and stages no LDS world at all (rtc_host.cpp plans it with none).
+constexpr bool kJitConstMaterials = kJitRecords;
+#endif
 
 // Visit every shape of kind K (wave-uniform loop, scalar loads).
 template <typename R, int K, typename F>
@@ -876,6 +881,19 @@ __device__ inline void jit_record_each(int slot, V3<float> p, V3<float>& w, int&
         jit_record_each<I + 1, E>(slot, p, w, mat);
     }
 }
+// ... and, for the direct kernel, the hit's material as constants too
+// (jit::kMaterials: registers instead of an LDS world and its staging)
+template <int I, int E>
+__device__ inline void jit_record_material_each(int slot, V3<float> p, V3<float>& w, MaterialRec<float>& mat) {
+    if constexpr (I < E) {
+        if (slot == I) {
+            const ShapeRec<float>& s = jit::kShapes[I];
+            w = xform_normal(s.inv, local_normal(s, jit_kind_of<I>(), xform_point(s.inv, p)));
+            mat = jit::kMaterials[s.material];
+        }
+        jit_record_material_each<I + 1, E>(slot, p, w, mat);
+    }
+}
 template <int I, int E>
 __device__ inline void jit_object_each(int slot, V3<float> p, V3<float>& obj) {
     if constexpr (I < E) {
@@ -1031,6 +1049,30 @@ struct Prepared {
     int mat;  // the hit's material index
 };
 
+#ifdef RTC_JIT
+// The per-scene direct kernel (no pool, few live values): prepare_hit with
+// the material as constants of the slot's branch (kJitConstMaterials).
+__device__ inline void prepare_hit_const(const DevScene<float>& sc, V3<float> o, V3<float> d, const Hit<float>& h,
+                                         Prepared<float>& q, bool& patterned, MaterialRec<float>& m) {
+    q.p = along(o, d, h.t);
+    V3<float> w = {0.0f, 0.0f, 0.0f};
+    jit_record_material_each<0, jit::kBegin[kNumKinds]>(h.slot, q.p, w, m);
+    asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(w.z));  // the hardware rsq, as hit_normal (bit for bit)
+    q.n = normalized(w);
+    q.eye = vneg(d);
+    if (dot(q.n, q.eye) < 0.0f) q.n = vneg(q.n);
+    q.mat = -1;  // (the direct kernel walks no refractive indices)
+    q.over = along(q.p, q.n, Real<float>::surface_offset(q.p.x, q.p.y, q.p.z));
+    q.base = {m.color[0], m.color[1], m.color[2]};
+    patterned = m.pattern >= 0;
+    if (jit::kPatterns && patterned) {
+        V3<float> obj = {0.0f, 0.0f, 0.0f};
+        jit_object_each<0, jit::kBegin[kNumKinds]>(h.slot, q.over, obj);
+        q.base = pattern_color_obj(sc, m.pattern, obj);
+    }
+}
+#endif
+
 template <typename R>
 __device__ inline const MaterialRec<R>& prepare_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, const Hit<R>& h,
                                                      Prepared<R>& q, bool& patterned) {
@@ -1130,7 +1172,19 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
     const Hit<R> h = closest_hit(sc, o, d);
     if (h.slot < 0) return false;  // world.rs:85: miss -> BLACK
     Prepared<R> q;
+#ifdef RTC_JIT
+    MaterialRec<R> m_const;
+    const MaterialRec<R>* mp;
+    if constexpr (kJitConstMaterials && !kChildren && sizeof(R) == 4) {
+        prepare_hit_const(sc, o, d, h, q, out.patterned, m_const);
+        mp = &m_const;
+    } else {
+        mp = &prepare_hit(sc, o, d, h, q, out.patterned);
+    }
+    const MaterialRec<R>& m = *mp;
+#else
     const MaterialRec<R>& m = prepare_hit(sc, o, d, h, q, out.patterned);
+#endif
     const V3<R> p = q.p, n = q.n, eye = q.eye, over = q.over, base = q.base;
     V3<R> surface = {(R)0, (R)0, (R)0};
     for_lights(sc, [&](const LightRec<R>& L) {

@@ -16,8 +16,8 @@ cp "$HPP" "$T/a/b/rtc_jit_scene.hpp"
 cp "$ROOT/ray-tracer-challenge-rs_amd/csrc/rtc_internal.hpp" "$T/a/b/"
 cp "$ROOT/include/rtc.h" "$T/include/"
 EXTRA_DEF=
-KERNEL="trace_pool<float, true, false>"
-case "$HPP" in *_direct.hpp) EXTRA_DEF=-DRTC_JIT_FENCE_EVERY=3; KERNEL="trace_direct<float, true>" ;; esac
+KERNEL=${JIT_KERNEL:-"trace_pool<float, true, false>"}
+case "$HPP" in *_direct.hpp) EXTRA_DEF=-DRTC_JIT_FENCE_EVERY=3; KERNEL=${JIT_KERNEL:-"trace_direct<float, false>"} ;; esac
 # hipRTC instantiates the kernel from its name expression; here explicitly
 { printf '#define RTC_JIT 1\n#include "rtc_jit_scene.hpp"\n'; cat "$ROOT/ray-tracer-challenge-rs_amd/csrc/rtc_kernels.hip"
   printf '\nnamespace rtc {\ntemplate __global__ void %s(LaunchParams<float>, RTC_WORLD_PARAMS(float));\n}\n' "$KERNEL"; } > "$T/a/b/k.hip"
