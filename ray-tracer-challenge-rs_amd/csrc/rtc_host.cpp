@@ -298,7 +298,7 @@ uint32_t pool_capacity(uint32_t depth, uint32_t batch) { return (uint32_t)kBlock
 
 template <typename R>
 size_t pool_lds_bytes(uint32_t cap) {
-    return 3 * kBlock * sizeof(PoolAcc<R>) + (size_t)cap * (7 * sizeof(R) + sizeof(uint32_t));
+    return 3 * kBlock * sizeof(PoolAcc<R>) + (size_t)cap * (7 * sizeof(R) + sizeof(PoolMeta));
 }
 
 // Scale of the f32 pool kernel's int32 pixel sums (rtc_internal.hpp
@@ -366,7 +366,7 @@ int pool_lds_rays(rt_context* ctx, uint32_t world_lds, uint32_t cap, uint32_t* l
     int best = 0, rc;
     if ((rc = blocks_per_cu<R>(ctx, true, lw, world_lds + pool_lds_bytes<R>(kBlock), &best))) return rc;
     if (best < 1) best = 1;
-    const size_t rec = 7 * sizeof(R) + sizeof(uint32_t);
+    const size_t rec = 7 * sizeof(R) + sizeof(PoolMeta);
     const size_t budget = (size_t)kLdsPerCu / (size_t)best;
     const size_t fixed = kStaticLds + world_lds + pool_lds_bytes<R>(0) + 511;
     uint32_t n = budget > fixed ? (uint32_t)((budget - fixed) / rec) : kBlock;

@@ -168,6 +168,14 @@ template <typename R>
 using PoolAcc = long long;
 #endif
 constexpr uint32_t kAccLog2Min = 8, kAccLog2Max = 28;
+// A pool entry's meta word (pixel | remaining << 8: 8 + 5 bits) as stored in
+// the LDS part of the pool; spilled entries keep 32 bits in their record.
+#ifndef RTC_POOL_META32  // (A/B builds: -DRTC_POOL_META32 keeps 32-bit entries)
+using PoolMeta = uint16_t;
+#else
+using PoolMeta = uint32_t;
+#endif
+static_assert(RT_MAX_SUPPORTED_DEPTH < 32, "remaining must fit the pool meta's 8 high bits");
 
 // ShapeRec::flags.  Value-equal shapes (shape_identity.hpp) form one identity
 // class; its members are adjacent within their kind's run of the table, the

@@ -1551,7 +1551,9 @@ __device__ inline void set_wave_prio(uint32_t p) {
 
 // Ray pool: a LIFO of pending rays per workgroup.  Slots [0, lds_cap) live
 // in dynamic LDS after the world tables:
-//   [acc: 3 x kBlock PoolAcc<R>][ox oy oz dx dy dz w : lds_cap x R][meta : lds_cap x u32]
+//   [acc: 3 x kBlock PoolAcc<R>][ox oy oz dx dy dz w : lds_cap x R][meta : lds_cap x u16]
+// (meta = pixel | remaining << 8 needs 13 bits; 16-bit entries give the pool
+// 1/16 more slots in the same LDS)
 // and slots [lds_cap, cap) in this workgroup's region of P.spill, one 8-word
 // record per entry (AoS: a lane's entry is two dwordx4 stores / loads in f32,
 // where the SoA layout took eight dword instructions per entry).  The LIFO bound cap = P + depth x
@@ -1670,7 +1672,7 @@ __device__ inline void pool_put(const Pool<R>& pl, int slot, V3<R> o, V3<R> d, R
 #endif
     if (slot < pl.lds_cap) {
         RTC_AS_LDS R* b = (RTC_AS_LDS R*)pl.lds;
-        pool_store<R>(b, (RTC_AS_LDS uint32_t*)(b + 7 * pl.lds_cap), pl.lds_cap, slot, o, d, w, meta);
+        pool_store<R>(b, (RTC_AS_LDS PoolMeta*)(b + 7 * pl.lds_cap), pl.lds_cap, slot, o, d, w, meta);
     } else {
         spill_store<R>((RTC_AS_GLOBAL R*)pl.spill + 8 * (size_t)(slot - pl.lds_cap), o, d, w, meta);
     }
@@ -1688,7 +1690,7 @@ __device__ inline void pool_get(const Pool<R>& pl, int slot, V3<R>& o, V3<R>& d,
 #endif
     if (slot < pl.lds_cap) {
         const RTC_AS_LDS R* b = (const RTC_AS_LDS R*)pl.lds;
-        pool_load<R>(b, (const RTC_AS_LDS uint32_t*)(b + 7 * pl.lds_cap), pl.lds_cap, slot, o, d, w, meta);
+        pool_load<R>(b, (const RTC_AS_LDS PoolMeta*)(b + 7 * pl.lds_cap), pl.lds_cap, slot, o, d, w, meta);
     } else {
         spill_load<R>((const RTC_AS_GLOBAL R*)pl.spill + 8 * (size_t)(slot - pl.lds_cap), o, d, w, meta);
     }
