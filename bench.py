@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--gather", choices=["rccl", "peer"], default="rccl",
                     help="tiled: how rank 0 gets the shards (rtc.h rt_context_set_gather); the other mode is "
                          "measured too and reported under gather_variants")
+    ap.add_argument("--ab", action="store_true",
+                    help="A/B runs: skip the one-shot child, the host-frame latency and the per-generation frame")
     ap.add_argument("--one-shot-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -520,6 +522,7 @@ def measure(args, tiled, world, rank, local):
                     ctx.upload(scene)
                     cold.append(timed_launches(step, stream, 1)())
                 line["cold_kernel_ms"] = float(np.median(cold))
+        if not tiled and world == 1 and not args.ab:
             # a drop-in Camera::render: synchronous rt_render into host memory,
             # PCIe copy included, into a canvas kept across frames (median of
             # 10; never `value`).  A canvas allocated per call adds its first-
@@ -551,7 +554,7 @@ def measure(args, tiled, world, rank, local):
                                           "shadow": [light_n * v for v in gen["shaded"]],
                                           "note": "generation g = bounce g (0 = camera rays); traced = radiance "
                                                   "rays (the wavefront), shadow = L per shaded hit"}
-        if world == 1 and not tiled:
+        if world == 1 and not tiled and not args.ab:
             line["one_shot"] = one_shot(args)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(scene, cam, args.depth, args.cpu_seconds)

@@ -47,6 +47,15 @@ def test_bench_line_contract():
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
     s0 = cb["configs0_serial"]  # BASELINE configs[0]: Camera::render at 320x240, one thread
     assert s0["cores"] == 1 and s0["ms_per_frame"] > 0 and s0["rays_per_frame"] == 2 * 320 * 240
+    # rays by kind and per generation
+    assert d["rays_by_kind"] == {"primary": 320 * 240, "shadow": 320 * 240, "reflect": 0, "refract": 0}
+    g = d["rays_by_generation"]
+    assert g["traced"][0] == g["shaded"][0] == g["shadow"][0] == 320 * 240 and sum(g["traced"][1:]) == 0
+    # the first frame and the one-shot (torch-free process) by phase
+    fb = d["first_frame_breakdown"]
+    assert {"scene_load_ms", "context_ms", "upload_ms", "first_render_ms", "d2h_ms"} <= set(fb)
+    os_ = d["one_shot"]
+    assert os_["total_ms"] >= os_["render_ms"] > 0 and os_["context_ms"] > 0, os_
 
 
 @pytest.mark.gpu
@@ -62,6 +71,11 @@ def test_bench_tiled_line_on_one_gpu():
     for k in ("render_ms_per_shard", "gather_ms", "frame_ms", "single_gpu_ms_per_step", "speedup_vs_1gpu"):
         assert d[k] > 0, k
     assert d["roofline"]["bound"] == "valu"
+    # both ways of assembling the frame on rank 0, measured over the same steps
+    gv = d["gather_variants"]
+    assert set(gv) == {"rccl", "peer"} and d["gather"] == "rccl"
+    for v in gv.values():
+        assert v["ms_per_step"] > 0 and v["frame_ms"] > 0 and v["render_ms_per_shard"] > 0
 
 
 @pytest.mark.gpu
