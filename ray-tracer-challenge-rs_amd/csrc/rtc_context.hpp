@@ -161,7 +161,7 @@ struct rt_context {
     bool jit_rejected[4] = {};   // built, but refused for occupancy or scratch (that variant only)
     bool jit_owner[4] = {};      // this context started the build: its time goes into jit_compile_ms
     uint32_t jit_frames = 0;     // large f32 frames of this upload so far (RT_JIT_AUTO starts at the 2nd)
-    std::string arch = "gfx950"; // the device's gfx target (hipDeviceProp_t::gcnArchName), for hipRTC
+    std::string arch;            // the device's gfx target (gcnArchName), for hipRTC; read lazily (device_arch)
     int jit_mode = 2;
     bool jit_failed = false, jit_used = false;  // jit_failed: the world's build failed (compile or load)
     double jit_compile_ms = 0;  // compile (or disk-cache load) time of this context's per-scene builds
@@ -249,6 +249,7 @@ unsigned long long timeout_ticks(double timeout_ms);
 constexpr uint32_t kJitMinTiles = 256;  // 64K pixels
 int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int static_blocks, hipFunction_t* fn);
 int jit_wait(rt_context* ctx, double timeout_ms, int* pending);
+const std::string& device_arch(rt_context* ctx);  // rtc_jit.cpp: the device's gfx target, read once
 
 // rtc_group.cpp: the same entry points on a multi-GPU context
 int group_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats,

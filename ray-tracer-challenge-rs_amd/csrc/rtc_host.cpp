@@ -857,15 +857,15 @@ int create_device_context(int device_ordinal, rt_context** out) {
     ctx->device = device_ordinal;
     RT_HIP(hipSetDevice(device_ordinal));
     tr.step("hipSetDevice");
-    hipDeviceProp_t prop;
-    RT_HIP(hipGetDeviceProperties(&prop, device_ordinal));
-    tr.step("hipGetDeviceProperties");
-    ctx->cu_count = prop.multiProcessorCount;
-    {  // "gfx950:sramecc+:xnack-" -> "gfx950": the per-scene builds' target
-        const std::string a(prop.gcnArchName);
-        if (!a.empty()) ctx->arch = a.substr(0, a.find(':'));
-    }
-    ctx->lds_per_block = prop.sharedMemPerBlock;  // launch limit of static + dynamic LDS
+    // two attributes instead of hipGetDeviceProperties (which fills every
+    // field of the struct); the gfx target for the per-scene builds is read
+    // when the first build needs it (device_arch, rtc_jit.cpp)
+    int cus = 0, lds = 0;
+    RT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_ordinal));
+    RT_HIP(hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device_ordinal));
+    tr.step("hipDeviceGetAttribute x2");
+    ctx->cu_count = cus;
+    ctx->lds_per_block = (size_t)lds;  // launch limit of static + dynamic LDS
     // scheduling knobs: "grid" (one workgroup per tile, the hardware dispatcher
     // balances), "static" (resident grid, fixed tile stride) or "dynamic"
     // (resident grid + per-XCD atomic tile queues)

@@ -366,6 +366,22 @@ void start_build(const std::shared_ptr<CodeBuild>& b, const jitfile::Request& rq
 
 }  // namespace
 
+// The device's gfx target ("gfx950:sramecc+:xnack-" -> "gfx950"), the
+// per-scene builds' --offload-arch: read at the first build, not at context
+// creation (hipGetDeviceProperties fills the whole struct).
+const std::string& device_arch(rt_context* ctx) {
+    if (ctx->arch.empty()) {
+        hipDeviceProp_t prop;
+        if (hipSetDevice(ctx->device) == hipSuccess && hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) {
+            const std::string a(prop.gcnArchName);
+            ctx->arch = a.empty() ? std::string("gfx950") : a.substr(0, a.find(':'));
+        } else {
+            ctx->arch = "gfx950";
+        }
+    }
+    return ctx->arch;
+}
+
 // The per-scene kernel for this context's uploaded world, or null (use the
 // generic kernel this launch).  RT_JIT_SYNC builds in line; RT_JIT_AUTO /
 // RT_JIT_EAGER start the build at the 2nd / 1st large frame of an upload and
@@ -390,7 +406,8 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
         table = fnv(traits, sizeof traits, table);
         // the device's gfx target: each build is compiled for one (make_request),
         // so devices of another target in the same process get builds of their own
-        table = fnv(ctx->arch.data(), ctx->arch.size() + 1, table);
+        const std::string& arch = device_arch(ctx);
+        table = fnv(arch.data(), arch.size() + 1, table);
         const uint32_t start_at = ctx->jit_mode == RT_JIT_AUTO ? 2 : 1;
         bool start = false;
         {
@@ -412,7 +429,7 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
                 make_request(scene_header(ctx->jit_shapes, ctx->jit_begin, ctx->jit_lights, ctx->jit_materials,
                                           ctx->jit_patterns,
                                           ctx->jit_pattern_kinds, ctx->jit_transparent),
-                             kernel_name(pool, lds), ctx->arch, &key);
+                             kernel_name(pool, lds), device_arch(ctx), &key);
             start_build(b, rq, key, sync);
         }
     }
