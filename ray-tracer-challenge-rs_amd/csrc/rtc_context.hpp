@@ -152,6 +152,7 @@ struct rt_context {
     std::vector<rtc::ShapeRec<float>> jit_shapes;
     std::vector<rtc::LightRec<float>> jit_lights;  // per-scene builds unroll the lights as constants
     std::vector<rtc::MaterialRec<float>> jit_materials;  // ... and the direct kernel reads materials as constants
+    std::vector<rtc::PatternRec<float>> jit_pattern_recs;  // (pattern kinds present)
     bool jit_patterns = true;                      // some material has a pattern (else pattern code is dropped)
     uint32_t jit_pattern_kinds = ~0u;              // pattern kinds in the world's table (bit per RT_PATTERN_*)
     bool jit_transparent = true;                   // some material is transparent (else no refraction code)
@@ -234,6 +235,7 @@ void scene_brightness(const rt_material_desc* mats, uint32_t nm, const rt_patter
                       const rt_light_desc* lights, uint32_t nl, double* bright_hit, double* bright_w);
 // One frame (or shard strip) of this device into `out_device` on `stream`.
 int capture_jit_table(rt_context* ctx);  // the f32 table of the uploaded world, for rtc_jit.cpp
+int fetch_jit_tables(rt_context* ctx);   // build_world<float>'s host tables read back (a group's other ranks)
 int launch_frame(rt_context* ctx, const rt_camera_desc* cam, const rt_render_options* o, uint32_t shard_index,
                  uint32_t shard_count, void* out_device, hipStream_t stream, bool image_rows = false);
 // Peer canvas internals (rtc_host.cpp): flags of a canvas, and the kernels.

@@ -370,7 +370,7 @@ int group_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns
         m->world_slot.assign(h.ns, 0);
         if (h.ns)
             RT_HIP(hipMemcpy(m->world_slot.data(), m->w32.world_slot, h.ns * sizeof(int32_t), hipMemcpyDeviceToHost));
-        if ((rc = capture_jit_table(m))) return rc;
+        if ((rc = fetch_jit_tables(m)) || (rc = capture_jit_table(m))) return rc;
         m->flops = FlopScene{};
         m->flops.per_ray = h.flops_per_ray;
         m->flops.n_lights = h.nl;

@@ -65,14 +65,18 @@ int set_error(int code, const std::string& msg) {
 namespace rtc {
 namespace {
 
+// Copies run on the context's stream, never the null stream: HIP creates a
+// hardware queue for the null stream at its first use, ~8 ms that a one-shot
+// render would pay.  The caller synchronizes the stream before
+// the host vector goes away.
 template <typename T>
-int upload(T** dst, const std::vector<T>& v) {
+int upload(T** dst, const std::vector<T>& v, hipStream_t s) {
     if (v.empty()) {
         *dst = nullptr;
         return RT_OK;
     }
     RT_HIP(hipMalloc(reinterpret_cast<void**>(dst), v.size() * sizeof(T)));
-    RT_HIP(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    RT_HIP(hipMemcpyAsync(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
     return RT_OK;
 }
 
@@ -248,9 +252,16 @@ int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes,
     put(pt.data(), pt.size() * sizeof(PatternRec<R>));
     put(ws.data(), ws.size() * sizeof(int32_t));
     RT_HIP(hipMalloc(&w.image, std::max<size_t>(image_bytes, 16)));  // (an empty world still gets a buffer)
-    if (image_bytes) RT_HIP(hipMemcpy(w.image, img.data(), image_bytes, hipMemcpyHostToDevice));
+    if (image_bytes) RT_HIP(hipMemcpyAsync(w.image, img.data(), image_bytes, hipMemcpyHostToDevice, ctx->stream));
     w.carve(sh.size(), nm, np);
-    if ((rc = upload(&w.lights, lt))) return rc;
+    if ((rc = upload(&w.lights, lt, ctx->stream))) return rc;
+    RT_HIP(hipStreamSynchronize(ctx->stream));  // (img and lt are host temporaries)
+    if constexpr (sizeof(R) == 4) {  // the per-scene build's tables (capture_jit_table), from the host copies
+        ctx->jit_shapes = sh;
+        ctx->jit_lights = lt;
+        ctx->jit_materials = mt;
+        ctx->jit_pattern_recs = pt;
+    }
     ctx->world_slot.assign(ws.begin(), ws.begin() + ns);
     w.scene.shapes = w.shapes;
     w.scene.materials = w.materials;
@@ -588,9 +599,10 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     // value-equal shapes (rt_scene_upload's identity classes) take the pool
     // kernel whose containers walk aggregates per class
     const bool dup = ctx->duplicate_shapes > 0;
-    // large f32 frames run the per-scene build of the same kernel (rtc_jit.cpp),
-    // planned with its own (smaller) LDS world when it takes the shape records
-    // from its instruction stream
+    // large f32 frames run the per-scene build of the same kernel (rtc_jit.cpp);
+    // a direct one takes the shape records and materials from its instruction
+    // stream and is planned with no LDS world (pool builds keep the LDS world:
+    // rtc_jit.cpp make_request)
     hipFunction_t jf = nullptr;
     if constexpr (sizeof(R) == 4) {
         const bool want = cam && !dup &&
@@ -599,7 +611,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
         if (want) {
             ++ctx->jit_frames;
             LaunchShape lj = ls;
-            if (ctx->lds_world && w.scene.kind_begin[kNumKinds] <= kJitRecordsMaxShapes &&
+            if (ctx->lds_world && !ls.pool && w.scene.kind_begin[kNumKinds] <= kJitRecordsMaxShapes &&
                 (rc = plan_launch<R>(ctx, w.scene, depth, P.n_tiles, lj, true)))
                 return rc;
             if ((rc = jit_function(ctx, lj.pool, lj.world_lds != 0, lj.lds, lj.per_cu, &jf))) return rc;
@@ -803,9 +815,10 @@ std::string device_error_text(int32_t err) {
 
 int check_pool_error(rt_context* ctx) {
     int32_t err = 0;
-    RT_HIP(hipMemcpy(&err, ctx->d_error, sizeof(err), hipMemcpyDeviceToHost));
+    RT_HIP(hipMemcpyAsync(&err, ctx->d_error, sizeof(err), hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(hipStreamSynchronize(ctx->stream));
     if (err) {
-        RT_HIP(hipMemset(ctx->d_error, 0, sizeof(int32_t)));
+        RT_HIP(hipMemsetAsync(ctx->d_error, 0, sizeof(int32_t), ctx->stream));
         return set_error(RT_ERR_POOL, device_error_text(err));
     }
     return RT_OK;
@@ -898,17 +911,19 @@ int create_device_context(int device_ordinal, rt_context** out) {
     const size_t qbytes = 2 * (size_t)kTileQueues * kQueueStride * sizeof(unsigned long long);  // two sets
     RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_tile_counter), qbytes));
     tr.step("hipMalloc");
-    RT_HIP(hipMemset(ctx->d_tile_counter, 0, qbytes));
-    tr.step("hipMemset (first)");
+    // (on the context's stream: the null stream's queue would cost ~8 ms more)
+    RT_HIP(hipMemsetAsync(ctx->d_tile_counter, 0, qbytes, ctx->stream));
+    tr.step("hipMemsetAsync (first)");
     const size_t counter_bytes = (size_t)kCounterShards * kNumCounters * sizeof(unsigned long long);
     RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_counters), counter_bytes));
-    RT_HIP(hipMemset(ctx->d_counters, 0, counter_bytes));
+    RT_HIP(hipMemsetAsync(ctx->d_counters, 0, counter_bytes, ctx->stream));
     RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_error), sizeof(int32_t)));
-    RT_HIP(hipMemset(ctx->d_error, 0, sizeof(int32_t)));
+    RT_HIP(hipMemsetAsync(ctx->d_error, 0, sizeof(int32_t), ctx->stream));
     const size_t gen_bytes = 2 * (size_t)kGenSlots * sizeof(unsigned long long);
     RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_gen_counts), gen_bytes));
-    RT_HIP(hipMemset(ctx->d_gen_counts, 0, gen_bytes));
-    tr.step("hipMalloc+hipMemset x3");
+    RT_HIP(hipMemsetAsync(ctx->d_gen_counts, 0, gen_bytes, ctx->stream));
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    tr.step("hipMalloc+hipMemsetAsync x3, sync");
     *out = ctx.release();
     return RT_OK;
 }
@@ -1013,25 +1028,33 @@ int build_scene(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const
     return RT_OK;
 }
 
+int fetch_jit_tables(rt_context* ctx) {
+    const DevScene<float>& sc = ctx->w32.scene;
+    ctx->jit_shapes.assign(sc.kind_begin[kNumKinds], ShapeRec<float>{});
+    ctx->jit_lights.assign(sc.n_lights, LightRec<float>{});
+    ctx->jit_materials.assign(sc.n_materials, MaterialRec<float>{});
+    ctx->jit_pattern_recs.assign(sc.n_patterns, PatternRec<float>{});
+    auto get = [&](auto& v, const void* src) -> hipError_t {
+        return v.empty() ? hipSuccess
+                         : hipMemcpyAsync(v.data(), src, v.size() * sizeof(v[0]), hipMemcpyDeviceToHost, ctx->stream);
+    };
+    RT_HIP(get(ctx->jit_shapes, ctx->w32.shapes));
+    RT_HIP(get(ctx->jit_lights, ctx->w32.lights));
+    RT_HIP(get(ctx->jit_materials, ctx->w32.materials));
+    RT_HIP(get(ctx->jit_pattern_recs, ctx->w32.patterns));
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
 int capture_jit_table(rt_context* ctx) {
-    const int32_t n = ctx->w32.scene.kind_begin[kNumKinds];
-    ctx->jit_shapes.assign(n, ShapeRec<float>{});
-    if (n) RT_HIP(hipMemcpy(ctx->jit_shapes.data(), ctx->w32.shapes, n * sizeof(ShapeRec<float>), hipMemcpyDeviceToHost));
+    // (jit_shapes, jit_lights, jit_materials, jit_pattern_recs: build_world<float>'s host tables)
     for (int k = 0; k <= kNumKinds; ++k) ctx->jit_begin[k] = ctx->w32.scene.kind_begin[k];
-    const int32_t nl = ctx->w32.scene.n_lights, nm = ctx->w32.scene.n_materials;
-    ctx->jit_lights.assign(nl, LightRec<float>{});
-    if (nl) RT_HIP(hipMemcpy(ctx->jit_lights.data(), ctx->w32.lights, nl * sizeof(LightRec<float>), hipMemcpyDeviceToHost));
-    std::vector<MaterialRec<float>> mats(nm);
-    if (nm) RT_HIP(hipMemcpy(mats.data(), ctx->w32.materials, nm * sizeof(MaterialRec<float>), hipMemcpyDeviceToHost));
-    ctx->jit_materials = mats;
+    const std::vector<MaterialRec<float>>& mats = ctx->jit_materials;
     ctx->jit_patterns = std::any_of(mats.begin(), mats.end(), [](const MaterialRec<float>& m) { return m.pattern >= 0; });
     ctx->jit_transparent =
         std::any_of(mats.begin(), mats.end(), [](const MaterialRec<float>& m) { return m.transparency != 0.0f; });
-    const int32_t np = ctx->w32.scene.n_patterns;
-    std::vector<PatternRec<float>> pats(np);
-    if (np) RT_HIP(hipMemcpy(pats.data(), ctx->w32.patterns, np * sizeof(PatternRec<float>), hipMemcpyDeviceToHost));
     ctx->jit_pattern_kinds = 0;
-    for (const PatternRec<float>& q : pats)  // every kind a pattern_color walk can meet (complex sub-patterns included)
+    for (const PatternRec<float>& q : ctx->jit_pattern_recs)  // every kind a pattern_color walk can meet (complex sub-patterns included)
         ctx->jit_pattern_kinds |= 1u << std::min<uint32_t>((uint32_t)q.kind, RT_PATTERN_TEST);
     for (int v = 0; v < 4; ++v) {
         ctx->jit_fn[v] = nullptr;
@@ -1263,7 +1286,8 @@ int rt_render(rt_context* ctx, const rt_camera_desc* cam, const rt_render_option
     float ms = 0.f;
     RT_HIP(hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_stop));
     if (*h_err) {
-        RT_HIP(hipMemset(ctx->d_error, 0, sizeof(int32_t)));
+        RT_HIP(hipMemsetAsync(ctx->d_error, 0, sizeof(int32_t), s));
+        RT_HIP(hipStreamSynchronize(s));
         return set_error(RT_ERR_POOL, device_error_text(*h_err));
     }
     if (stats) {

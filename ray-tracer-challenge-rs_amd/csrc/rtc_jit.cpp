@@ -219,6 +219,12 @@ jitfile::Request make_request(const std::string& scene, const char* name, const 
     // -3.6 %, three_sphere 4K -2.5 %, 1080p -0.6 %; the pool kernel lost 15 %
     // on cover that way and keeps a fence per shape.
     if (!std::strstr(name, "pool")) rq.opts.push_back("-DRTC_JIT_FENCE_EVERY=3");
+    // Shape records as constants (rtc_kernels.hip kJitRecords) pay off in the
+    // direct kernel only.  Same-box A/B, two rounds (profiles/r04_ab_builds.log):
+    // direct three_sphere 17.0 us with them vs 18.4 us without; pool kernels
+    // without them reflect_refract -3.0 %, table -1.2 %, cover -0.6 % (the
+    // per-slot branches cost more than the extra LDS pool slots gain).
+    else rq.opts.push_back("-DRTC_JIT_NO_RECORDS");
     // RTC_JIT_FLAGS: extra compiler options, space- or comma-separated (A/B diagnostics)
     if (const char* e = std::getenv("RTC_JIT_FLAGS")) {
         const std::string all(e);

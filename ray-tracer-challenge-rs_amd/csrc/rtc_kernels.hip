@@ -431,9 +431,10 @@ __device__ inline void jit_each(F&& f) {
 // hit's shape record from the instruction stream: the hit's slot rides in
 // the closest-hit key next to its world index, and its normal, material and
 // pattern-space point come from one branch per slot present among the
-// wave's hits, where the record is constants (jit_record_each).  Their LDS
-// then holds only the materials and patterns (rtc_host.cpp
-// jit_world_lds_bytes), which leaves more of it to the ray pool.
+// wave's hits, where the record is constants (jit_record_each).  Only the
+// direct kernel is built so (rtc_jit.cpp make_request passes
+// RTC_JIT_NO_RECORDS to pool builds, which measured faster with the records
+// in LDS).
 #if defined(RTC_JIT) && !defined(RTC_JIT_NO_RECORDS)
 constexpr bool kJitRecords = jit::kBegin[kNumKinds] <= 255;  // rtc_host.cpp kJitRecordsMaxShapes
 #else

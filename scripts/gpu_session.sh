@@ -6,6 +6,7 @@
 #   smoke    __graft_entry__.smoke()
 #   bench    bench.py with the driver's flags, then 1000 steps; f64 line
 #   pool     bench lines of the pool configs (reflect_refract, cover/table 4K)
+#   initprobe  start-up step timings of a bare HIP process      -> gpurun_out/initprobe.log
 #   prof     rocprofv3 --kernel-trace --stats of the bench     -> gpurun_out/prof_*
 # Usage: scripts/gpu_session.sh tests smoke bench ...
 set -u
@@ -65,6 +66,13 @@ for step in "$@"; do
         RTC_TRACE_INIT=1 timeout -k 10 120 python bench.py --one-shot-child > gpurun_out/oneshot_$i.log 2>&1
         rc=$?; echo "oneshot rc=$rc"; grep -v amdgpu.ids gpurun_out/oneshot_$i.log; [ $rc -eq 0 ] || exit $rc
       done ;;
+    initprobe)  # start-up steps of a bare HIP process (scripts/init_probe.cpp), with and without RCCL loaded
+      : > gpurun_out/initprobe.log
+      for a in ${PROBES:-"" "rccl" "" "rccl" "prefault=touch" "prefault=huge" "prefault=threads" "prefault=small" "prefault=register"}; do
+        timeout -k 10 60 scripts/_init_probe $a >> gpurun_out/initprobe.log 2>&1
+        rc=$?; [ $rc -eq 0 ] || { echo "initprobe $a rc=$rc"; exit $rc; }
+      done
+      cat gpurun_out/initprobe.log ;;
     prof)
       for sc in three_sphere_scene reflect_refract; do
         timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$sc -o run -- \
