@@ -605,8 +605,11 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     // rtc_jit.cpp make_request)
     hipFunction_t jf = nullptr;
     if constexpr (sizeof(R) == 4) {
-        const bool want = cam && !dup &&
-                          !(flags & (RT_FLAG_STAMPS | RT_FLAG_NO_SHADE | RT_FLAG_NO_TRACE | RT_FLAG_GENERATIONS)) &&
+        // (the per-scene pool kernel keeps the stamps and item log: a stamped
+        // launch times the kernel a warm renderer runs; the direct one has none)
+        const uint32_t generic_only =
+            RT_FLAG_NO_SHADE | RT_FLAG_NO_TRACE | RT_FLAG_GENERATIONS | (ls.pool ? 0u : RT_FLAG_STAMPS);
+        const bool want = cam && !dup && !(flags & generic_only) &&
                           (ctx->jit_mode == RT_JIT_SYNC || (ctx->jit_mode >= RT_JIT_AUTO && P.n_tiles >= kJitMinTiles));
         if (want) {
             ++ctx->jit_frames;

@@ -7,6 +7,9 @@
 #   bench    bench.py with the driver's flags, then 1000 steps; f64 line
 #   pool     bench lines of the pool configs (reflect_refract, cover/table 4K)
 #   initprobe  start-up step timings of a bare HIP process      -> gpurun_out/initprobe.log
+#   shards   per-shard kernel times (scripts/shard_times.py)  -> gpurun_out/shards.log
+#   shardtail  item log of one 8-way shard at split 8 and 16 -> gpurun_out/shardtail.log
+#   profset  the round's profile set (scripts/profile_round.sh)  -> gpurun_out/r04_*
 #   prof     rocprofv3 --kernel-trace --stats of the bench     -> gpurun_out/prof_*
 # Usage: scripts/gpu_session.sh tests smoke bench ...
 set -u
@@ -73,6 +76,23 @@ for step in "$@"; do
         rc=$?; [ $rc -eq 0 ] || { echo "initprobe $a rc=$rc"; exit $rc; }
       done
       cat gpurun_out/initprobe.log ;;
+    shards)  # per-shard kernel time at N = 1 and 8 (what each rank renders), cover and table 4K
+      : > gpurun_out/shards.log
+      for sc in cover table; do
+        SHARD_COUNTS=${SHARD_COUNTS:-1,8} timeout -k 10 300 python scripts/shard_times.py $sc 3840 2160 >> gpurun_out/shards.log 2>&1
+        rc=$?; [ $rc -eq 0 ] || { echo "shards $sc rc=$rc"; tail -5 gpurun_out/shards.log; exit $rc; }
+      done
+      grep -v amdgpu.ids gpurun_out/shards.log ;;
+    shardtail)  # item log of shard 0 of 8 (cover 4K) at split 8 and 16
+      : > gpurun_out/shardtail.log
+      for sm in 3 4; do
+        RTC_SPLIT_MAX=$sm timeout -k 10 300 python scripts/shard_tail.py cover 3840 2160 8 0 >> gpurun_out/shardtail.log 2>&1
+        rc=$?; [ $rc -eq 0 ] || { echo "shardtail rc=$rc"; tail -5 gpurun_out/shardtail.log; exit $rc; }
+      done
+      grep -v amdgpu.ids gpurun_out/shardtail.log | cut -c1-1500 ;;
+    profset)  # the round's profile set (scripts/profile_round.sh; ROUND, default r04)
+      ROUND=${ROUND:-r04} bash scripts/profile_round.sh > gpurun_out/profset.log 2>&1
+      rc=$?; echo "profset rc=$rc"; grep -v amdgpu.ids gpurun_out/profset.log | cut -c1-400 | tail -40; [ $rc -eq 0 ] || exit $rc ;;
     prof)
       for sc in three_sphere_scene reflect_refract; do
         timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$sc -o run -- \

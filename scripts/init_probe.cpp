@@ -3,7 +3,7 @@
 // it, and the first device-to-host copy into an untouched pageable canvas with
 // several ways of faulting its pages in first.  Diagnostic only.
 //   hipcc -O2 -o scripts/_init_probe scripts/init_probe.cpp -ldl -lpthread
-//   scripts/_init_probe [rccl] [prefault=none|touch|huge|threads|small|register]
+//   scripts/_init_probe [rccl] [prefault=none|touch|huge|threads|small|register|blit]
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 #include <sys/mman.h>
@@ -42,6 +42,9 @@ int main(int argc, char** argv) {
         if (!std::strcmp(argv[i], "rccl")) rccl = true;
         if (!std::strncmp(argv[i], "prefault=", 9)) prefault = argv[i] + 9;
     }
+    // blit: the runtime's copy-engine threshold raised before it starts, so the
+    // canvas copy runs as a blit kernel on the compute queue instead of SDMA
+    if (prefault == "blit") setenv("GPU_FORCE_BLIT_COPY_SIZE", "1048576", 1);
     std::printf("init_probe rccl=%d prefault=%s\n", rccl, prefault.c_str());
     g_t0 = g_t = clk::now();
     if (rccl) {
