@@ -577,6 +577,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
         P.tiles_x = (cam->width + RT_TILE_W - 1) / RT_TILE_W;
         P.tile_rows = tile_rows_for(cam->height, shard_count, shard_index);
         P.n_tiles = P.tiles_x * P.tile_rows;
+        P.tiles_x_magic = div_magic(P.tiles_x, P.n_tiles);
     } else {
         P.rays = d_rays;
         P.n_rays = n_rays;

@@ -131,6 +131,20 @@ constexpr int32_t kErrPeerTimeout = 64;  // rt_canvas_wait: a shard's flag did n
 // Peer canvas (rt_canvas_create): the W x H image and, after it at this
 // alignment, one u64 completion flag per shard.
 constexpr uint64_t kCanvasFlagAlign = 256;
+// t / d for every t < n as one multiply-high by m = ceil(2^32 / d): with
+// m d = 2^32 + e, 0 <= e < d, t m / 2^32 = t/d + t e / (d 2^32), and the
+// second term stays below 1/d (so below the gap to the next integer) while
+// n d < 2^32.  Returns 0 where that does not hold (divide instead).  The
+// tracer kernels take the tile row of tile t this way (LaunchParams::
+// tiles_x_magic): one s_mul_hi_u32 instead of a ~25-instruction division.
+RTC_HD inline uint32_t div_magic(uint32_t d, uint32_t n) {
+    if (d < 2 || (uint64_t)n * d >= (1ull << 32)) return 0;
+    return (uint32_t)(((1ull << 32) + d - 1) / d);
+}
+RTC_HD inline uint32_t div_by(uint32_t t, uint32_t d, uint32_t magic) {
+    return magic ? (uint32_t)(((uint64_t)t * magic) >> 32) : t / d;
+}
+
 RTC_HD inline uint64_t canvas_flag_offset(uint64_t image_bytes) {
     return (image_bytes + kCanvasFlagAlign - 1) / kCanvasFlagAlign * kCanvasFlagAlign;
 }
@@ -292,7 +306,7 @@ struct LaunchParams {
     uint32_t world_lds;      // bytes of world tables staged at the start of dynamic LDS (0 = none)
     void* spill;                 // pool overflow: grid x 8 x (pool_capacity - pool_lds_capacity) words
     uint32_t spill_blocks;       // workgroups the spill buffer holds regions for (RTC_BOUNDS_CHECK)
-    uint32_t pad_spill;
+    uint32_t tiles_x_magic;      // div_magic(tiles_x, n_tiles): tile row = div_by(t, tiles_x, magic)
     unsigned long long* stamps;  // RT_FLAG_STAMPS: 2 x grid s_memrealtime values
     unsigned long long* item_log;  // RT_FLAG_STAMPS pool launches: [0] count, then 3 x u64 per item
     unsigned long long* tile_counter;  // kTileQueues queue heads, kQueueStride apart (zero at launch)

@@ -1306,7 +1306,7 @@ static_assert(RT_TILE_W % RTC_WAVE_W == 0 && RT_TILE_H % (64 / RTC_WAVE_W) == 0,
 template <typename R>
 __device__ inline bool tile_pixel(const LaunchParams<R>& P, uint32_t t, uint32_t tid, uint32_t& x, uint32_t& y,
                                   uint64_t& out_idx) {
-    const uint32_t lrow = t / P.tiles_x, tcol = t - lrow * P.tiles_x;
+    const uint32_t lrow = div_by(t, P.tiles_x, P.tiles_x_magic), tcol = t - lrow * P.tiles_x;
     // wave w of the tile covers one RTC_WAVE_W x (64 / RTC_WAVE_W) pixel block
     constexpr uint32_t kPerRow = RT_TILE_W / RTC_WAVE_W, kWaveH = 64 / RTC_WAVE_W;
     const uint32_t wave = tid / 64, lane = tid % 64;

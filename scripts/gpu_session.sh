@@ -76,11 +76,15 @@ for step in "$@"; do
         rc=$?; [ $rc -eq 0 ] || { echo "initprobe $a rc=$rc"; exit $rc; }
       done
       cat gpurun_out/initprobe.log ;;
-    shards)  # per-shard kernel time at N = 1 and 8 (what each rank renders), cover and table 4K
+    shards)  # per-shard kernel time at N = 1 and 8 (what each rank renders), cover and table 4K;
+             # SHARD_ENVS: environment settings to sweep ("-" = none)
       : > gpurun_out/shards.log
-      for sc in cover table; do
-        SHARD_COUNTS=${SHARD_COUNTS:-1,8} timeout -k 10 300 python scripts/shard_times.py $sc 3840 2160 >> gpurun_out/shards.log 2>&1
-        rc=$?; [ $rc -eq 0 ] || { echo "shards $sc rc=$rc"; tail -5 gpurun_out/shards.log; exit $rc; }
+      for e in ${SHARD_ENVS:--}; do
+        for sc in cover table; do
+          [ "$e" = - ] || echo "$e" >> gpurun_out/shards.log
+          env ${e/#-/} SHARD_COUNTS=${SHARD_COUNTS:-1,8} timeout -k 10 300 python scripts/shard_times.py $sc 3840 2160 >> gpurun_out/shards.log 2>&1
+          rc=$?; [ $rc -eq 0 ] || { echo "shards $sc rc=$rc"; tail -5 gpurun_out/shards.log; exit $rc; }
+        done
       done
       grep -v amdgpu.ids gpurun_out/shards.log ;;
     shardtail)  # item log of shard 0 of 8 (cover 4K) at split 8 and 16

@@ -30,6 +30,26 @@ int main() {
                     const WorkItem w = decode_item(item, true);
                     CHECK(w.tile == t && w.part == p && w.split_log2 == l && w.prio == pr);
                 }
+    // tile rows by multiply-high (div_magic / div_by): exhaustive over small
+    // divisors, then every t near a multiple of d for large ones up to the
+    // validity limit n d < 2^32, and the fallback where it does not hold
+    for (uint32_t d = 1; d <= 130; ++d) {
+        const uint32_t n = d * 40000u, m = div_magic(d, n);
+        CHECK((d < 2) == (m == 0));
+        for (uint32_t t = 0; t < n; ++t) CHECK(div_by(t, d, m) == t / d);
+    }
+    for (uint32_t d : {131u, 240u, 255u, 256u, 257u, 1000u, 4095u, 65535u, 65536u, 100003u}) {
+        const uint32_t n = (uint32_t)(((1ull << 32) - 1) / d);  // largest n with n d < 2^32
+        const uint32_t m = div_magic(d, n);
+        CHECK(m != 0 && div_magic(d, n + 1) == 0);
+        for (uint64_t q = 0; q * d < n; q += 1 + q / 64)
+            for (int64_t k = -2; k <= 2; ++k) {
+                const int64_t t = (int64_t)(q * d) + k;
+                if (t >= 0 && t < (int64_t)n) CHECK(div_by((uint32_t)t, d, m) == (uint32_t)t / d);
+            }
+        CHECK(div_by(n - 1, d, m) == (n - 1) / d);
+        CHECK(div_by(12345u, d, 0) == 12345u / d);
+    }
     // raster items are plain tiles at every size (rt_color_at: up to 2^24 tiles)
     for (uint32_t t : {0u, kItemTileMask, kItemTileMask + 1u, 0x1234567u, 0xFFFFFFu, 0xFFFFFFFEu}) {
         const WorkItem w = decode_item(t, false);
