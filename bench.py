@@ -201,6 +201,9 @@ def one_shot_child(args):
     synchronous rt_render into a host canvas (the cold generic kernel, module
     load and PCIe copy included).  Prints one JSON object."""
     os.environ["RTC_NO_TORCH"] = "1"
+    # the CLI's setting (rtc_cli.cpp main, INTEGRATION.md): frame copies as blit
+    # kernels, not on an SDMA engine whose first use costs 8-12 ms
+    os.environ.setdefault("GPU_FORCE_BLIT_COPY_SIZE", "1048576")
     import numpy as np
     import rtc_amd
     from rtc_amd import scene_io
@@ -225,15 +228,16 @@ def one_shot_child(args):
     ctx.close()
 
 
-def one_shot(args):
-    """Run one_shot_child in a subprocess (rank 0, N = 1); None if it fails."""
+def one_shot(args, env=None):
+    """Run one_shot_child in a subprocess (rank 0, N = 1); None if it fails.
+    `env`: extra environment of the child (the SDMA-copy variant)."""
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--one-shot-child", "--precision", args.precision]
     for k in ("scene", "width", "height", "depth"):
         if getattr(args, k) is not None:
             cmd += [f"--{k}", str(getattr(args, k))]
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env={**os.environ, **(env or {})})
         lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
         return json.loads(lines[-1]) if r.returncode == 0 and lines else {"error": (r.stderr or r.stdout)[-400:]}
     except Exception as e:  # noqa: BLE001  (a diagnostic: never fails the bench line)
@@ -556,6 +560,8 @@ def measure(args, tiled, world, rank, local):
                                                   "rays (the wavefront), shadow = L per shaded hit"}
         if world == 1 and not tiled and not args.ab:
             line["one_shot"] = one_shot(args)
+            # the same with the runtime's default copy engine (SDMA) for the frame copy
+            line["one_shot_sdma_copy"] = one_shot(args, {"GPU_FORCE_BLIT_COPY_SIZE": "0"})
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(scene, cam, args.depth, args.cpu_seconds)
             line["cpu_baseline"]["configs0_serial"] = cpu_serial_configs0(min(3.0, args.cpu_seconds / 4))

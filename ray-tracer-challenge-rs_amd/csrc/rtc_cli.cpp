@@ -30,6 +30,13 @@ static int usage() {
 
 int main(int argc, char** argv) {
     if (argc < 3) return usage();
+    // A one-shot process copies one frame back: the HIP runtime's first
+    // copy on an SDMA engine costs 8-12 ms of engine set-up, a blit kernel
+    // on the compute queue ~2.4 ms for the same 24.9 MB (DESIGN.md §5,
+    // scripts/init_probe.cpp).  Read when the runtime starts (the first HIP
+    // call, in rt_context_create); a value already in the environment wins.
+    setenv("GPU_FORCE_BLIT_COPY_SIZE", "1048576", 0);  // KiB: every copy below 1 GiB
+
     const char* scene_path = argv[1];
     const char* out_path = argv[2];
     bool quiet = false, ppm_binary = false, timings = false;
