@@ -534,7 +534,10 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
             (void)hipFree(ctx->d_cold_order);
             ctx->d_cold_order = nullptr;
             RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_cold_order), v.size() * sizeof(uint32_t)));
-            RT_HIP(hipMemcpy(ctx->d_cold_order, v.data(), v.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+            // (the launch's stream, not the null stream; v is a host temporary)
+            RT_HIP(hipMemcpyAsync(ctx->d_cold_order, v.data(), v.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                  stream));
+            RT_HIP(hipStreamSynchronize(stream));
             ctx->cold_w = P.width;
             ctx->cold_h = P.height;
         }

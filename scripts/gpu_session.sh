@@ -56,6 +56,20 @@ for step in "$@"; do
           done
         done
       done ;;
+    abenv)  # environment knobs on this build (scripts/ab_env.sh): AB_SCENES, AB_ENVS (space-separated, X=0 = default)
+      timeout -k 10 1000 bash scripts/ab_env.sh "${AB_SCENES:-reflect_refract}" ${AB_ENVS:-X=0} > gpurun_out/abenv.log 2>&1
+      rc=$?; echo "abenv rc=$rc"; cat gpurun_out/abenv.log; [ $rc -eq 0 ] || exit $rc ;;
+    coldtail)  # item logs of a cold and a warm launch (scripts/cold_tail.py)
+      : > gpurun_out/coldtail.log
+      for a in "reflect_refract 1920 1080" "cover 3840 2160"; do
+        timeout -k 10 200 python scripts/cold_tail.py $a >> gpurun_out/coldtail.log 2>&1
+        rc=$?; [ $rc -eq 0 ] || { echo "coldtail rc=$rc"; tail -5 gpurun_out/coldtail.log; exit $rc; }
+      done
+      grep -v amdgpu.ids gpurun_out/coldtail.log | cut -c1-2500 ;;
+    partest)  # one test file (PARTEST, default the parity tests)
+      timeout -k 10 600 python -u -m pytest ${PARTEST:-tests/test_gpu_parity.py} -m gpu -q --timeout 300 --timeout-method thread \
+        -p no:cacheprovider > gpurun_out/partest.log 2>&1
+      rc=$?; echo "partest rc=$rc"; tail -15 gpurun_out/partest.log; ok $rc || exit $rc ;;
     jitdump)  # per-scene headers of the bench scenes for scripts/jit_isa.sh
       mkdir -p gpurun_out/jit
       for a in "--scene three_sphere_scene" "--scene reflect_refract" "--scene cover --width 3840 --height 2160" \

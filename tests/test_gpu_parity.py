@@ -240,19 +240,17 @@ def test_split_tiles_are_exact(rtc, monkeypatch, name, shard):
     splits nearly every tile 4 (RTC_SPLIT_MAX=3: 8, 4: 16) ways, at 1 every tile above the mean load),
     then the frozen order reused (launches 4 and 5): every render equals the
     raster-ordered one bit for bit, counters included.  The first launch runs
-    the order of the cold-frame cost probe (split too in the last case), the
-    costliest items at raised wave priority."""
+    the centre-out cold order, later ones the costliest items at raised wave
+    priority."""
     scene = scene_fixture(name)
     cam = rtc.camera_resize(scene.camera, 256, 160)
     rows = rtc.shard_rows(cam.height, shard[1])
     raster, s0 = _render_with_env(rtc, monkeypatch, {"RTC_TILE_ORDER": "0"}, scene, cam, "f32")
     raster = raster[:rows] if shard[1] == 1 else None
-    for split, most, probe in (("0.0001", "2", "8,24"), ("1", "2", "8,24"), ("0.0001", "3", "8,24,1"),
-                                 ("0.0001", "4", "8,24,1"), ("1", "4", "8,24")):
+    for split, most in (("0.0001", "2"), ("1", "2"), ("0.0001", "3"), ("0.0001", "4"), ("1", "4")):
         monkeypatch.setenv("RTC_TILE_ORDER", "1")
         monkeypatch.setenv("RTC_SPLIT", split)
         monkeypatch.setenv("RTC_SPLIT_MAX", most)  # up to 4, 8 (half-wave seeds) or 16 parts (wave-row seeds)
-        monkeypatch.setenv("RTC_COLD_PROBE", probe)
         with rtc.Context(0) as c:
             c.upload(scene)
             first, s1 = c.render(cam, 6, precision="f32", shard=shard)
