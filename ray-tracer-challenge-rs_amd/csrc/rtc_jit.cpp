@@ -32,7 +32,9 @@
 #include <hip/hiprtc.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
+#include <cmath>
 #include <cerrno>
 #include <chrono>
 #include <condition_variable>
@@ -91,6 +93,93 @@ std::string floats(const float (&a)[N]) {
     for (size_t i = 0; i < N; ++i) s += (i ? ", " : "") + hexf(a[i]);
     return s + "}";
 }
+std::string ball4(const float* a) {  // a cluster ball: 4 floats
+    std::string s = "{";
+    for (size_t i = 0; i < 4; ++i) s += (i ? ", " : "") + hexf(a[i]);
+    return s + "}";
+}
+
+// Clusters of the world's bounded shapes for the per-scene kernels' two-level
+// wave cull (rtc_kernels.hip for_all_culled): a wave that meets no lane's ray
+// with a cluster's ball skips all its members' tests.  k-means on the bound
+// centres (k ~ sqrt(n), 2..6, farthest-point seeds: deterministic), each
+// cluster's ball enclosing its members' padded balls.  Worlds of fewer than
+// kClusterMinShapes bounded shapes get none (RTC_JIT_CLUSTERS=0: never; =k:
+// k clusters, for sweeps).
+constexpr int kClusterMinShapes = 6;
+struct Clusters {
+    std::vector<std::array<float, 4>> ball;  // centre, radius^2
+    std::vector<int> begin, members, unclustered;
+};
+Clusters make_clusters(const std::vector<ShapeRec<float>>& sh) {
+    Clusters c;
+    std::vector<int> bounded;
+    for (int i = 0; i < (int)sh.size(); ++i) {
+        const float r2 = sh[i].bound[3];
+        if (std::isfinite(r2) && r2 >= 0.0f) bounded.push_back(i);
+        else c.unclustered.push_back(i);
+    }
+    const char* e = std::getenv("RTC_JIT_CLUSTERS");
+    const int n = (int)bounded.size();
+    if (n < kClusterMinShapes || (e && !std::strcmp(e, "0"))) {
+        c.unclustered.insert(c.unclustered.end(), bounded.begin(), bounded.end());
+        std::sort(c.unclustered.begin(), c.unclustered.end());
+        c.begin = {0};
+        return c;
+    }
+    int k = std::min(6, std::max(2, (int)std::lround(std::sqrt((double)n))));
+    if (e && std::atoi(e) >= 2) k = std::min(n, std::atoi(e));
+    auto ctr = [&](int i) { return std::array<double, 3>{sh[i].bound[0], sh[i].bound[1], sh[i].bound[2]}; };
+    auto d2 = [](const std::array<double, 3>& a, const std::array<double, 3>& b) {
+        return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
+    };
+    std::vector<std::array<double, 3>> cent{ctr(bounded[0])};
+    while ((int)cent.size() < k) {  // farthest point from the seeds so far
+        int far = bounded[0];
+        double best = -1.0;
+        for (int i : bounded) {
+            double m = 1e300;
+            for (const auto& q : cent) m = std::min(m, d2(ctr(i), q));
+            if (m > best) best = m, far = i;
+        }
+        cent.push_back(ctr(far));
+    }
+    std::vector<int> lab(n, 0);
+    for (int it = 0; it < 32; ++it) {
+        for (int j = 0; j < n; ++j) {
+            double m = 1e300;
+            for (int q = 0; q < k; ++q)
+                if (const double v = d2(ctr(bounded[j]), cent[q]); v < m) m = v, lab[j] = q;
+        }
+        for (int q = 0; q < k; ++q) {
+            std::array<double, 3> sum{0, 0, 0};
+            int cnt = 0;
+            for (int j = 0; j < n; ++j)
+                if (lab[j] == q) {
+                    const auto a = ctr(bounded[j]);
+                    for (int t = 0; t < 3; ++t) sum[t] += a[t];
+                    ++cnt;
+                }
+            if (cnt) cent[q] = {sum[0] / cnt, sum[1] / cnt, sum[2] / cnt};
+        }
+    }
+    c.begin.push_back(0);
+    for (int q = 0; q < k; ++q) {
+        double r = 0.0;
+        int cnt = 0;
+        for (int j = 0; j < n; ++j)
+            if (lab[j] == q) {
+                c.members.push_back(bounded[j]);
+                r = std::max(r, std::sqrt(d2(ctr(bounded[j]), cent[q])) + std::sqrt((double)sh[bounded[j]].bound[3]));
+                ++cnt;
+            }
+        if (!cnt) continue;
+        const double pad = 1e-4 * (r + std::fabs(cent[q][0]) + std::fabs(cent[q][1]) + std::fabs(cent[q][2])) + 1e-4;
+        c.ball.push_back({(float)cent[q][0], (float)cent[q][1], (float)cent[q][2], (float)((r + pad) * (r + pad))});
+        c.begin.push_back((int)c.members.size());
+    }
+    return c;
+}
 
 // rtc_jit_scene.hpp: the world's f32 shape table, its lights and whether any
 // material has a pattern, as constexpr data.
@@ -107,6 +196,22 @@ std::string scene_header(const std::vector<ShapeRec<float>>& sh, const int32_t b
              ", " + hexf(r.ymin) + ", " + hexf(r.ymax) + ", " + floats(r.tri) + "},\n";
     }
     s += "    {}};\n";
+    const Clusters cl = make_clusters(sh);
+    auto ints = [](const std::vector<int>& v) {
+        std::string o = "{";
+        for (size_t i = 0; i < v.size(); ++i) o += (i ? ", " : "") + std::to_string(v[i]);
+        return o + (v.empty() ? "0}" : "}");
+    };
+    s += "constexpr int kNumClusters = " + std::to_string(cl.ball.size()) + ";\n";
+    s += "constexpr float kClusterBall[" + std::to_string(cl.ball.size() + 1) + "][4] = {\n";
+    for (const auto& b : cl.ball) s += "    " + ball4(b.data()) + ",\n";
+    s += "    {}};\n";
+    s += "constexpr int kClusterBegin[" + std::to_string(cl.begin.size()) + "] = " + ints(cl.begin) + ";\n";
+    s += "constexpr int kClusterMembers[" + std::to_string(std::max<size_t>(1, cl.members.size())) + "] = " +
+         ints(cl.members) + ";\n";
+    s += "constexpr int kNumUnclustered = " + std::to_string(cl.unclustered.size()) + ";\n";
+    s += "constexpr int kUnclustered[" + std::to_string(std::max<size_t>(1, cl.unclustered.size())) + "] = " +
+         ints(cl.unclustered) + ";\n";
     s += "constexpr int kNumLights = " + std::to_string(lights.size()) + ";\n";
     s += "constexpr LightRec<float> kLights[" + std::to_string(lights.size() + 1) + "] = {\n";
     for (const LightRec<float>& l : lights) s += "    {" + floats(l.position) + ", " + floats(l.intensity) + "},\n";

@@ -504,24 +504,32 @@ __device__ inline bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) 
 // dd = dot(d, d), formed once per ray by the caller: in the per-scene build
 // the ray fence between unrolled shapes would otherwise recompute it for
 // every shape.
-template <typename R, int K>
-__device__ inline bool wave_may_hit(const ShapeRec<R>& s, V3<R> o, V3<R> d, R dd) {
-    if constexpr (K == RT_SHAPE_PLANE) return true;
-    const R r2 = s.bound[3];  // radius^2
-    if constexpr (K != RT_SHAPE_SPHERE && K != RT_SHAPE_CUBE)
-        if (!(r2 >= (R)0)) return true;  // unbounded shape: wave-uniform
-    const V3<R> oc = {s.bound[0] - o.x, s.bound[1] - o.y, s.bound[2] - o.z};
+// The ball test itself, for a shape's bound or (per-scene builds) a cluster
+// of shapes' (for_all_culled): kHalfLine = t >= 0 only, else the whole line.
+template <typename R, bool kHalfLine>
+__device__ inline bool wave_ball_may_hit(R cx, R cy, R cz, R r2, V3<R> o, V3<R> d, R dd) {
+    const V3<R> oc = {cx - o.x, cy - o.y, cz - o.z};
     // |d x oc|^2 = |oc|^2 |d|^2 - (oc.d)^2 (Lagrange): reuses oc.d of the
     // front test.  Rounding of the two products is bounded by ~12 ulp of
     // |oc|^2 |d|^2; shrinking |oc|^2 by 1 - kKeep (>> that) keeps the test
     // conservative, so no lane that meets the sphere is ever rejected.
     constexpr R kKeep = sizeof(R) == 4 ? (R)(1 - 1e-5) : (R)(1 - 1e-12);
     const R tc = dot(oc, d), oo = dot(oc, oc);
+    if constexpr (!kHalfLine) return wave_any(Real<R>::madd(oo, kKeep, -r2) * dd <= tc * tc);
     // front = tc >= 0 | oo <= r2, lane = front & line test: one ballot per
     // comparison, combined as SGPR masks (a ballot of the combined bool makes
     // the compiler materialise it in a VGPR and compare it again: 2 VALU)
     const unsigned long long front = __builtin_amdgcn_ballot_w64(tc >= (R)0) | __builtin_amdgcn_ballot_w64(oo <= r2);
     return (front & __builtin_amdgcn_ballot_w64(Real<R>::madd(oo, kKeep, -r2) * dd <= tc * tc)) != 0;
+}
+
+template <typename R, int K>
+__device__ inline bool wave_may_hit(const ShapeRec<R>& s, V3<R> o, V3<R> d, R dd) {
+    if constexpr (K == RT_SHAPE_PLANE) return true;
+    const R r2 = s.bound[3];  // radius^2
+    if constexpr (K != RT_SHAPE_SPHERE && K != RT_SHAPE_CUBE)
+        if (!(r2 >= (R)0)) return true;  // unbounded shape: wave-uniform
+    return wave_ball_may_hit<R, true>(s.bound[0], s.bound[1], s.bound[2], r2, o, d, dd);
 }
 
 // The refractive-index walk's cull: entries at every t count there (t < 0
@@ -539,10 +547,7 @@ __device__ inline bool wave_line_may_hit(const ShapeRec<R>& s, V3<R> o, V3<R> d,
     const R r2 = s.bound[3];
     if constexpr (K != RT_SHAPE_SPHERE && K != RT_SHAPE_CUBE)
         if (!(r2 >= (R)0)) return true;
-    const V3<R> oc = {s.bound[0] - o.x, s.bound[1] - o.y, s.bound[2] - o.z};
-    constexpr R kKeep = sizeof(R) == 4 ? (R)(1 - 1e-5) : (R)(1 - 1e-12);
-    const R tc = dot(oc, d), oo = dot(oc, oc);
-    return wave_any(Real<R>::madd(oo, kKeep, -r2) * dd <= tc * tc);
+    return wave_ball_may_hit<R, false>(s.bound[0], s.bound[1], s.bound[2], r2, o, d, dd);
 }
 
 // Per-scene build only: the ray's registers pass through an empty asm at the
@@ -559,6 +564,62 @@ __device__ inline void jit_fence(V3<R>& o, V3<R>& d, int slot = 0) {
         if (slot % RTC_JIT_FENCE_EVERY == 0)
             asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z), "+v"(d.x), "+v"(d.y), "+v"(d.z));
 #endif
+}
+
+// Every shape, as for_all_kinds, but per-scene builds of worlds with shape
+// clusters (rtc_jit.cpp make_clusters) visit them cluster by cluster: a
+// cluster's members only when some active lane's ray (kHalfLine) or line may
+// meet the cluster's ball, which encloses every member's own padded ball, so
+// a skipped member's own cull would have skipped it too.  Unclustered shapes
+// (unbounded ones) are visited first.  The visit order differs from the table
+// order; every caller's result is order-independent (closest hit by (t, world)
+// key, any-hit by minimum, the walk per shape).
+#ifdef RTC_JIT
+constexpr int jit_kind_of(int slot) {
+    int k = 0;
+    while (k < kNumKinds - 1 && slot >= jit::kBegin[k + 1]) ++k;
+    return k;
+}
+template <int M, typename F>
+__device__ inline void jit_unclustered(F&& f) {
+    if constexpr (M < jit::kNumUnclustered) {
+        constexpr int slot = jit::kUnclustered[M];
+        f.template operator()<jit_kind_of(slot)>(jit::kShapes[slot], slot);
+        jit_unclustered<M + 1>(f);
+    }
+}
+template <int C, int M, typename F>
+__device__ inline void jit_members(F&& f) {
+    if constexpr (M < jit::kClusterBegin[C + 1]) {
+        constexpr int slot = jit::kClusterMembers[M];
+        f.template operator()<jit_kind_of(slot)>(jit::kShapes[slot], slot);
+        jit_members<C, M + 1>(f);
+    }
+}
+template <bool kHalfLine, int C, typename F>
+__device__ inline void jit_clusters(V3<float>& o, V3<float>& d, float dd, F&& f) {
+    if constexpr (C < jit::kNumClusters) {
+        jit_fence(o, d);
+        if (wave_ball_may_hit<float, kHalfLine>(jit::kClusterBall[C][0], jit::kClusterBall[C][1], jit::kClusterBall[C][2],
+                                                jit::kClusterBall[C][3], o, d, dd))
+            jit_members<C, jit::kClusterBegin[C]>(f);
+        jit_clusters<kHalfLine, C + 1>(o, d, dd, f);
+    }
+}
+#endif
+template <typename R, bool kHalfLine, typename F>
+__device__ inline void for_all_culled(const DevScene<R>& sc, V3<R>& o, V3<R>& d, R dd, F&& f) {
+#ifdef RTC_JIT
+    if constexpr (sizeof(R) == 4 && jit::kNumClusters > 0) {
+        jit_unclustered<0>(f);
+        jit_clusters<kHalfLine, 0>(o, d, dd, f);
+        return;
+    }
+#endif
+    (void)o;
+    (void)d;
+    (void)dd;
+    for_all_kinds<R>(sc, f);
 }
 
 template <typename R>
@@ -628,7 +689,7 @@ template <typename R>
 __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
     Nearest<R> best;
     const R dd = dot(d, d);
-    for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
+    for_all_culled<R, true>(sc, o, d, dd, [&]<int K>(const ShapeRec<R>& s, int slot) {
         jit_fence(o, d, slot);
         if (!wave_may_hit<R, K>(s, o, d, dd)) return;
         const V3<R> lo = xform_point(s.inv, o);
@@ -673,7 +734,7 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) 
 #endif
     Blocker<R> b;
     const R dd = dot(d, d);
-    for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
+    for_all_culled<R, true>(sc, o, d, dd, [&]<int K>(const ShapeRec<R>& s, int slot) {
         if (!s.casts_shadow) return;  // wave-uniform
         jit_fence(o, d, slot);
         if (!wave_may_hit<R, K>(s, o, d, dd)) return;
@@ -777,9 +838,16 @@ __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> 
             settle(count, last, s, (uint32_t)s.flags >> kShapeClassShift == hit_class);
             count = 0;
         });
+    } else if constexpr (kWalkCull) {  // (line culls: clusters too in per-scene builds)
+        for_all_culled<R, false>(sc, o, d, dd, [&]<int K>(const ShapeRec<R>& s, int slot) {
+            if (!wave_line_may_hit<R, K>(s, o, d, dd)) return;  // no entries: nothing to settle
+            int count = 0;
+            Key last{};
+            scan.template operator()<K>(s, count, last);
+            settle(count, last, s, slot == h.slot);
+        });
     } else {
         for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {
-            if (kWalkCull && !wave_line_may_hit<R, K>(s, o, d, dd)) return;  // no entries: nothing to settle
             int count = 0;
             Key last{};
             scan.template operator()<K>(s, count, last);
