@@ -102,10 +102,10 @@ std::string ball4(const float* a) {  // a cluster ball: 4 floats
 // Clusters of the world's bounded shapes for the per-scene kernels' two-level
 // wave cull (rtc_kernels.hip for_all_culled): a wave that meets no lane's ray
 // with a cluster's ball skips all its members' tests.  k-means on the bound
-// centres (k ~ sqrt(n), 2..6, farthest-point seeds: deterministic), each
-// cluster's ball enclosing its members' padded balls.  Worlds of fewer than
-// kClusterMinShapes bounded shapes get none (RTC_JIT_CLUSTERS=0: never; =k:
-// k clusters, for sweeps).
+// centres (farthest-point seeds: deterministic; k from 2 to 8 by the cost
+// model below), each cluster's ball enclosing its members' padded balls.
+// Worlds of fewer than kClusterMinShapes bounded shapes get none
+// (RTC_JIT_CLUSTERS=0: never; =k: k clusters, for sweeps).
 constexpr int kClusterMinShapes = 6;
 struct Clusters {
     std::vector<std::array<float, 4>> ball;  // centre, radius^2
@@ -121,61 +121,93 @@ Clusters make_clusters(const std::vector<ShapeRec<float>>& sh) {
     }
     const char* e = std::getenv("RTC_JIT_CLUSTERS");
     const int n = (int)bounded.size();
-    if (n < kClusterMinShapes || (e && !std::strcmp(e, "0"))) {
+    auto flat = [&]() {
         c.unclustered.insert(c.unclustered.end(), bounded.begin(), bounded.end());
         std::sort(c.unclustered.begin(), c.unclustered.end());
+        c.ball.clear();
+        c.members.clear();
         c.begin = {0};
         return c;
-    }
-    int k = std::min(6, std::max(2, (int)std::lround(std::sqrt((double)n))));
-    if (e && std::atoi(e) >= 2) k = std::min(n, std::atoi(e));
-    auto ctr = [&](int i) { return std::array<double, 3>{sh[i].bound[0], sh[i].bound[1], sh[i].bound[2]}; };
-    auto d2 = [](const std::array<double, 3>& a, const std::array<double, 3>& b) {
+    };
+    if (n < kClusterMinShapes || (e && !std::strcmp(e, "0"))) return flat();
+    using P3 = std::array<double, 3>;
+    auto ctr = [&](int i) { return P3{sh[i].bound[0], sh[i].bound[1], sh[i].bound[2]}; };
+    auto rad = [&](int i) { return std::sqrt((double)sh[i].bound[3]); };
+    auto d2 = [](const P3& a, const P3& b) {
         return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
     };
-    std::vector<std::array<double, 3>> cent{ctr(bounded[0])};
-    while ((int)cent.size() < k) {  // farthest point from the seeds so far
-        int far = bounded[0];
-        double best = -1.0;
-        for (int i : bounded) {
-            double m = 1e300;
-            for (const auto& q : cent) m = std::min(m, d2(ctr(i), q));
-            if (m > best) best = m, far = i;
+    struct Cl {
+        P3 cent;
+        double r;
+        std::vector<int> m;
+    };
+    auto kmeans = [&](int k) {
+        std::vector<P3> cent{ctr(bounded[0])};
+        while ((int)cent.size() < k) {  // farthest point from the seeds so far
+            int far = bounded[0];
+            double best = -1.0;
+            for (int i : bounded) {
+                double m = 1e300;
+                for (const auto& q : cent) m = std::min(m, d2(ctr(i), q));
+                if (m > best) best = m, far = i;
+            }
+            cent.push_back(ctr(far));
         }
-        cent.push_back(ctr(far));
-    }
-    std::vector<int> lab(n, 0);
-    for (int it = 0; it < 32; ++it) {
-        for (int j = 0; j < n; ++j) {
-            double m = 1e300;
-            for (int q = 0; q < k; ++q)
-                if (const double v = d2(ctr(bounded[j]), cent[q]); v < m) m = v, lab[j] = q;
+        std::vector<int> lab(n, 0);
+        for (int it = 0; it < 32; ++it) {
+            for (int j = 0; j < n; ++j) {
+                double m = 1e300;
+                for (int q = 0; q < k; ++q)
+                    if (const double v = d2(ctr(bounded[j]), cent[q]); v < m) m = v, lab[j] = q;
+            }
+            for (int q = 0; q < k; ++q) {
+                P3 sum{0, 0, 0};
+                int cnt = 0;
+                for (int j = 0; j < n; ++j)
+                    if (lab[j] == q) {
+                        const P3 a = ctr(bounded[j]);
+                        for (int t = 0; t < 3; ++t) sum[t] += a[t];
+                        ++cnt;
+                    }
+                if (cnt) cent[q] = {sum[0] / cnt, sum[1] / cnt, sum[2] / cnt};
+            }
         }
+        std::vector<Cl> out;
         for (int q = 0; q < k; ++q) {
-            std::array<double, 3> sum{0, 0, 0};
-            int cnt = 0;
+            Cl cl{cent[q], 0.0, {}};
             for (int j = 0; j < n; ++j)
                 if (lab[j] == q) {
-                    const auto a = ctr(bounded[j]);
-                    for (int t = 0; t < 3; ++t) sum[t] += a[t];
-                    ++cnt;
+                    cl.m.push_back(bounded[j]);
+                    cl.r = std::max(cl.r, std::sqrt(d2(ctr(bounded[j]), cent[q])) + rad(bounded[j]));
                 }
-            if (cnt) cent[q] = {sum[0] / cnt, sum[1] / cnt, sum[2] / cnt};
+            if (!cl.m.empty()) out.push_back(cl);
         }
+        return out;
+    };
+    // k by a cost model: cull tests per ray = one per cluster plus the members
+    // of each cluster a ray meets, taken as (cluster radius / world radius)^2;
+    // no clusters unless that beats testing every bounded shape by 20 %
+    P3 mid{0, 0, 0};
+    for (int i : bounded)
+        for (int t = 0; t < 3; ++t) mid[t] += ctr(i)[t] / n;
+    double world = 0.0;
+    for (int i : bounded) world = std::max(world, std::sqrt(d2(ctr(i), mid)) + rad(i));
+    std::vector<Cl> best;
+    double best_cost = 0.8 * n;
+    const int forced = e ? std::atoi(e) : 0;
+    for (int k = 2; k <= std::min(8, n - 1); ++k) {
+        if (forced >= 2 && k != std::min(forced, n - 1)) continue;
+        std::vector<Cl> cl = kmeans(k);
+        double cost = (double)cl.size();
+        for (const Cl& q : cl) cost += (double)q.m.size() * std::min(1.0, (q.r / world) * (q.r / world));
+        if (cost < best_cost || forced >= 2) best_cost = cost, best = std::move(cl);
     }
+    if (best.empty()) return flat();
     c.begin.push_back(0);
-    for (int q = 0; q < k; ++q) {
-        double r = 0.0;
-        int cnt = 0;
-        for (int j = 0; j < n; ++j)
-            if (lab[j] == q) {
-                c.members.push_back(bounded[j]);
-                r = std::max(r, std::sqrt(d2(ctr(bounded[j]), cent[q])) + std::sqrt((double)sh[bounded[j]].bound[3]));
-                ++cnt;
-            }
-        if (!cnt) continue;
-        const double pad = 1e-4 * (r + std::fabs(cent[q][0]) + std::fabs(cent[q][1]) + std::fabs(cent[q][2])) + 1e-4;
-        c.ball.push_back({(float)cent[q][0], (float)cent[q][1], (float)cent[q][2], (float)((r + pad) * (r + pad))});
+    for (const Cl& q : best) {
+        c.members.insert(c.members.end(), q.m.begin(), q.m.end());
+        const double pad = 1e-4 * (q.r + std::fabs(q.cent[0]) + std::fabs(q.cent[1]) + std::fabs(q.cent[2])) + 1e-4;
+        c.ball.push_back({(float)q.cent[0], (float)q.cent[1], (float)q.cent[2], (float)((q.r + pad) * (q.r + pad))});
         c.begin.push_back((int)c.members.size());
     }
     return c;
