@@ -105,7 +105,8 @@ std::string ball4(const float* a) {  // a cluster ball: 4 floats
 // centres (farthest-point seeds: deterministic; k from 2 to 8 by the cost
 // model below), each cluster's ball enclosing its members' padded balls.
 // Worlds of fewer than kClusterMinShapes bounded shapes get none
-// (RTC_JIT_CLUSTERS=0: never; =k: k clusters, for sweeps).
+// (RTC_JIT_CLUSTERS=0: never; =k: k clusters, for sweeps; =1: one cluster of
+// every bounded shape, from two shapes on).
 constexpr int kClusterMinShapes = 6;
 struct Clusters {
     std::vector<std::array<float, 4>> ball;  // centre, radius^2
@@ -129,7 +130,8 @@ Clusters make_clusters(const std::vector<ShapeRec<float>>& sh) {
         c.begin = {0};
         return c;
     };
-    if (n < kClusterMinShapes || (e && !std::strcmp(e, "0"))) return flat();
+    const int forced = e ? std::atoi(e) : 0;
+    if ((n < kClusterMinShapes && !(forced >= 1 && n >= 2)) || (e && !std::strcmp(e, "0"))) return flat();
     using P3 = std::array<double, 3>;
     auto ctr = [&](int i) { return P3{sh[i].bound[0], sh[i].bound[1], sh[i].bound[2]}; };
     auto rad = [&](int i) { return std::sqrt((double)sh[i].bound[3]); };
@@ -194,13 +196,12 @@ Clusters make_clusters(const std::vector<ShapeRec<float>>& sh) {
     for (int i : bounded) world = std::max(world, std::sqrt(d2(ctr(i), mid)) + rad(i));
     std::vector<Cl> best;
     double best_cost = 0.8 * n;
-    const int forced = e ? std::atoi(e) : 0;
-    for (int k = 2; k <= std::min(8, n - 1); ++k) {
-        if (forced >= 2 && k != std::min(forced, n - 1)) continue;
+    for (int k = forced == 1 ? 1 : 2; k <= std::min(8, n - 1); ++k) {
+        if (forced >= 1 && k != std::min(forced, n - 1)) continue;
         std::vector<Cl> cl = kmeans(k);
         double cost = (double)cl.size();
         for (const Cl& q : cl) cost += (double)q.m.size() * std::min(1.0, (q.r / world) * (q.r / world));
-        if (cost < best_cost || forced >= 2) best_cost = cost, best = std::move(cl);
+        if (cost < best_cost || forced >= 1) best_cost = cost, best = std::move(cl);
     }
     if (best.empty()) return flat();
     c.begin.push_back(0);
