@@ -109,7 +109,6 @@ std::string ball4(const float* a) {  // a cluster ball: 4 floats
 // every bounded shape, from two shapes on).
 constexpr int kClusterMinShapes = 6;
 struct Clusters {
-    std::array<float, 4> root{0, 0, 0, -1};  // ball of every cluster (radius^2 < 0: no root test)
     std::vector<std::array<float, 4>> ball;  // centre, radius^2
     std::vector<int> begin, members, unclustered;
 };
@@ -205,11 +204,6 @@ Clusters make_clusters(const std::vector<ShapeRec<float>>& sh) {
         if (cost < best_cost || forced >= 1) best_cost = cost, best = std::move(cl);
     }
     if (best.empty()) return flat();
-    // a root ball over all clusters, tested first (RTC_JIT_ROOT=0: none)
-    if (const char* r = std::getenv("RTC_JIT_ROOT"); !(r && !std::strcmp(r, "0"))) {
-        const double pad = 1e-4 * (world + std::fabs(mid[0]) + std::fabs(mid[1]) + std::fabs(mid[2])) + 1e-4;
-        c.root = {(float)mid[0], (float)mid[1], (float)mid[2], (float)((world + pad) * (world + pad))};
-    }
     c.begin.push_back(0);
     for (const Cl& q : best) {
         c.members.insert(c.members.end(), q.m.begin(), q.m.end());
@@ -242,7 +236,6 @@ std::string scene_header(const std::vector<ShapeRec<float>>& sh, const int32_t b
         return o + (v.empty() ? "0}" : "}");
     };
     s += "constexpr int kNumClusters = " + std::to_string(cl.ball.size()) + ";\n";
-    s += "constexpr float kClusterRoot[4] = " + ball4(cl.root.data()) + ";\n";
     s += "constexpr float kClusterBall[" + std::to_string(cl.ball.size() + 1) + "][4] = {\n";
     for (const auto& b : cl.ball) s += "    " + ball4(b.data()) + ",\n";
     s += "    {}};\n";

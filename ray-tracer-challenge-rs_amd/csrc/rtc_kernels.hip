@@ -612,13 +612,6 @@ __device__ inline void for_all_culled(const DevScene<R>& sc, V3<R>& o, V3<R>& d,
 #ifdef RTC_JIT
     if constexpr (sizeof(R) == 4 && jit::kNumClusters > 0) {
         jit_unclustered<0>(f);
-        // the root ball holds every cluster: a wave that misses it skips them all
-        if constexpr (jit::kClusterRoot[3] >= 0.0f) {
-            jit_fence(o, d);
-            if (!wave_ball_may_hit<float, kHalfLine>(jit::kClusterRoot[0], jit::kClusterRoot[1], jit::kClusterRoot[2],
-                                                     jit::kClusterRoot[3], o, d, dd))
-                return;
-        }
         jit_clusters<kHalfLine, 0>(o, d, dd, f);
         return;
     }

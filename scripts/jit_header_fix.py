@@ -66,7 +66,6 @@ if "kNumClusters" not in text:
         return "__builtin_bit_cast(float, 0x%08xu)" % struct.unpack("<I", struct.pack("<f", v))[0]
     ints = lambda v: "{" + ", ".join(map(str, v or [0])) + "}"  # noqa: E731
     add = "constexpr int kNumClusters = %d;\n" % len(balls)
-    add += "constexpr float kClusterRoot[4] = {%s};\n" % ", ".join(f(x) for x in [0.0, 0.0, 0.0, -1.0])
     add += "constexpr float kClusterBall[%d][4] = {\n%s    {}};\n" % (
         len(balls) + 1, "".join("    {%s},\n" % ", ".join(f(x) for x in b) for b in balls))
     add += "constexpr int kClusterBegin[%d] = %s;\n" % (len(begin), ints(begin))
