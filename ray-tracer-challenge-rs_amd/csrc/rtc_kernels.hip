@@ -596,29 +596,39 @@ __device__ inline void jit_members(F&& f) {
         jit_members<C, M + 1>(f);
     }
 }
-template <bool kHalfLine, int C, typename F>
-__device__ inline void jit_clusters(V3<float>& o, V3<float>& d, float dd, F&& f) {
+template <bool kHalfLine, int C, typename F, typename S>
+__device__ inline void jit_clusters(V3<float>& o, V3<float>& d, float dd, F&& f, S&& skip) {
     if constexpr (C < jit::kNumClusters) {
         jit_fence(o, d);
-        if (wave_ball_may_hit<float, kHalfLine>(jit::kClusterBall[C][0], jit::kClusterBall[C][1], jit::kClusterBall[C][2],
+        if (!skip(jit::kClusterBall[C][0], jit::kClusterBall[C][1], jit::kClusterBall[C][2], jit::kClusterBall[C][3]) &&
+            wave_ball_may_hit<float, kHalfLine>(jit::kClusterBall[C][0], jit::kClusterBall[C][1], jit::kClusterBall[C][2],
                                                 jit::kClusterBall[C][3], o, d, dd))
             jit_members<C, jit::kClusterBegin[C]>(f);
-        jit_clusters<kHalfLine, C + 1>(o, d, dd, f);
+        jit_clusters<kHalfLine, C + 1>(o, d, dd, f, skip);
     }
 }
 #endif
-template <typename R, bool kHalfLine, typename F>
-__device__ inline void for_all_culled(const DevScene<R>& sc, V3<R>& o, V3<R>& d, R dd, F&& f) {
+// `skip(centre, r^2)`: a caller's wave-uniform reason to pass a cluster by
+// before its ball test (none by default).
+struct NoSkip {
+    template <typename... A>
+    __device__ bool operator()(A...) const {
+        return false;
+    }
+};
+template <typename R, bool kHalfLine, typename F, typename S = NoSkip>
+__device__ inline void for_all_culled(const DevScene<R>& sc, V3<R>& o, V3<R>& d, R dd, F&& f, S&& skip = S{}) {
 #ifdef RTC_JIT
     if constexpr (sizeof(R) == 4 && jit::kNumClusters > 0) {
         jit_unclustered<0>(f);
-        jit_clusters<kHalfLine, 0>(o, d, dd, f);
+        jit_clusters<kHalfLine, 0>(o, d, dd, f, skip);
         return;
     }
 #endif
     (void)o;
     (void)d;
     (void)dd;
+    (void)skip;
     for_all_kinds<R>(sc, f);
 }
 
@@ -734,6 +744,10 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) 
 #endif
     Blocker<R> b;
     const R dd = dot(d, d);
+    // once every active lane is blocked the remaining clusters cannot change
+    // the answer (per cluster, not per shape: a per-shape check measured
+    // slower in round 3; per cluster cover -2.5 %, cylinders -4 %, table +1 %)
+    auto skip = [&](R, R, R, R) { return !wave_any(!b.blocked(dist)); };
     for_all_culled<R, true>(sc, o, d, dd, [&]<int K>(const ShapeRec<R>& s, int slot) {
         if (!s.casts_shadow) return;  // wave-uniform
         jit_fence(o, d, slot);
@@ -741,7 +755,7 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) 
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
         entries<R, K>(s, lo, ld, [&](R t, bool v) { b.offer(t, v, dist); });
-    });
+    }, skip);
     return b.blocked(dist);
 }
 
