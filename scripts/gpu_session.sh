@@ -108,6 +108,9 @@ for step in "$@"; do
         rc=$?; [ $rc -eq 0 ] || { echo "shardtail rc=$rc"; tail -5 gpurun_out/shardtail.log; exit $rc; }
       done
       grep -v amdgpu.ids gpurun_out/shardtail.log | cut -c1-1500 ;;
+    roundbench)  # the round's bench lines (scripts/round_bench.sh; ROUND, default r04)
+      ROUND=${ROUND:-r04} timeout -k 10 1000 bash scripts/round_bench.sh > gpurun_out/roundbench.log 2>&1
+      rc=$?; echo "roundbench rc=$rc"; cat gpurun_out/roundbench.log | cut -c1-300; [ $rc -eq 0 ] || exit $rc ;;
     profset)  # the round's profile set (scripts/profile_round.sh; ROUND, default r04)
       ROUND=${ROUND:-r04} bash scripts/profile_round.sh > gpurun_out/profset.log 2>&1
       rc=$?; echo "profset rc=$rc"; grep -v amdgpu.ids gpurun_out/profset.log | cut -c1-400 | tail -40; [ $rc -eq 0 ] || exit $rc ;;
