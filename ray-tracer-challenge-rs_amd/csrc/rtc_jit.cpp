@@ -198,11 +198,52 @@ Clusters make_clusters(const std::vector<ShapeRec<float>>& sh) {
     double world = 0.0;
     for (int i : bounded) world = std::max(world, std::sqrt(d2(ctr(i), mid)) + rad(i));
     constexpr double kMemberWeight = 2.0;
+    // k-means groups by centre only; a local search then moves single shapes
+    // between clusters while that lowers the model's cost (sum over clusters of
+    // members x radius^2), which k-means cannot see: a large shape pulls its
+    // cluster's ball wide (RTC_JIT_CLUSTER_REFINE=0: k-means only)
+    const char* rf = std::getenv("RTC_JIT_CLUSTER_REFINE");
+    const bool refine = !(rf && !std::strcmp(rf, "0"));
+    auto ball_of = [&](Cl& q) {
+        q.cent = {0, 0, 0};
+        for (int i : q.m)
+            for (int t = 0; t < 3; ++t) q.cent[t] += ctr(i)[t] / (double)q.m.size();
+        q.r = 0.0;
+        for (int i : q.m) q.r = std::max(q.r, std::sqrt(d2(ctr(i), q.cent)) + rad(i));
+    };
+    auto term = [&](const Cl& q) { return (double)q.m.size() * q.r * q.r; };
+    auto refine_clusters = [&](std::vector<Cl>& cl) {
+        for (int guard = 0; guard < 256; ++guard) {
+            double best_gain = 1e-9 * world * world;
+            int ba = -1, bs = -1, bb = -1;
+            for (int a = 0; a < (int)cl.size(); ++a) {
+                if (cl[a].m.size() < 2) continue;
+                for (int si = 0; si < (int)cl[a].m.size(); ++si)
+                    for (int b = 0; b < (int)cl.size(); ++b) {
+                        if (b == a) continue;
+                        Cl na = cl[a], nb = cl[b];
+                        na.m.erase(na.m.begin() + si);
+                        nb.m.push_back(cl[a].m[si]);
+                        ball_of(na);
+                        ball_of(nb);
+                        const double gain = term(cl[a]) + term(cl[b]) - term(na) - term(nb);
+                        if (gain > best_gain) best_gain = gain, ba = a, bs = si, bb = b;
+                    }
+            }
+            if (ba < 0) break;
+            cl[bb].m.push_back(cl[ba].m[bs]);
+            cl[ba].m.erase(cl[ba].m.begin() + bs);
+            ball_of(cl[ba]);
+            ball_of(cl[bb]);
+        }
+        for (Cl& q : cl) std::sort(q.m.begin(), q.m.end());
+    };
     std::vector<Cl> best;
     double best_cost = 0.8 * kMemberWeight * n;
     for (int k = forced == 1 ? 1 : 2; k <= std::min(8, n - 1); ++k) {
         if (forced >= 1 && k != std::min(forced, n - 1)) continue;
         std::vector<Cl> cl = kmeans(k);
+        if (refine) refine_clusters(cl);
         double cost = (double)cl.size();
         for (const Cl& q : cl) cost += kMemberWeight * (double)q.m.size() * std::min(1.0, (q.r / world) * (q.r / world));
         if (cost < best_cost || forced >= 1) best_cost = cost, best = std::move(cl);
