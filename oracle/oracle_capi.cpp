@@ -198,13 +198,3 @@ int orc_last_generations(uint64_t* traced, uint64_t* shaded) {
 }
 
 }  // extern "C"
-
-#ifdef ORC_CHECK_SELF_SHADOW
-// Test infrastructure: shadow tests eligible for the GPU self-skip, and those
-// where the hit's own shape was the only blocker (rtc_oracle.hpp shade_hit).
-extern "C" int orc_self_shadow_counts(uint64_t* checked, uint64_t* violations) {
-    if (checked) *checked = World::self_shadow_checked;
-    if (violations) *violations = World::self_shadow_violations;
-    return 0;
-}
-#endif

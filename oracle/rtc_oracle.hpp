@@ -765,36 +765,12 @@ struct World {
             if (x.shape->material.casts_shadow && x.t >= 0.0 && x.t < dist) return true;
         return false;
     }
-#ifdef ORC_CHECK_SELF_SHADOW
-    // Test infrastructure (tests/test_shadow_self_skip.py): the GPU kernels skip
-    // the hit's own shape in a shadow test when it is flat (plane, triangle) or
-    // convex (sphere, cube) and seen from outside, and the light is on the
-    // normal's side.  Count the shadow tests where that shape is the only
-    // blocker the reference finds: any would make the skip inexact.
-    static inline uint64_t self_shadow_checked = 0, self_shadow_violations = 0;
-#endif
     // world.rs:38-67
     Color shade_hit(const Comps& c, Hits& xs, int remaining, Counters* k = nullptr) const {
         const Material& m = c.shape->material;
         Color surface = BLACK;
         for (const Light& l : lights) {
             bool shadowed = is_in_shadow(l, c.over_point, xs);
-#ifdef ORC_CHECK_SELF_SHADOW
-            {
-                const int kd = c.shape->kind;
-                const bool flat = kd == S_PLANE || kd == S_TRIANGLE;
-                const bool skippable = flat || ((kd == S_SPHERE || kd == S_CUBE) && !c.inside);
-                const Vector lv = sub(l.position, c.over_point);
-                const double dist = magnitude(lv);
-                if (skippable && dot(normalized(lv), c.normal) >= 0.0) {
-                    __atomic_add_fetch(&self_shadow_checked, 1, __ATOMIC_RELAXED);
-                    bool own = false, other = false;
-                    for (const Hit& x : xs)
-                        if (x.shape->material.casts_shadow && x.t >= 0.0 && x.t < dist) (x.shape == c.shape ? own : other) = true;
-                    if (own && !other) __atomic_add_fetch(&self_shadow_violations, 1, __ATOMIC_RELAXED);
-                }
-            }
-#endif
             if (k) {
                 k->shadow++;
                 if (m.pattern) k->lit_patterned++;

@@ -632,20 +632,6 @@ __device__ inline void for_all_culled(const DevScene<R>& sc, V3<R>& o, V3<R>& d,
     for_all_kinds<R>(sc, f);
 }
 
-// The kind of the shape in table slot `slot` (the table is sorted by kind).
-template <typename R>
-__device__ inline int slot_kind(const DevScene<R>& sc, int slot) {
-    int k = 0;
-#ifdef RTC_JIT
-    if constexpr (sizeof(R) == 4) {
-        for (int i = 1; i < kNumKinds; ++i) k += slot >= jit::kBegin[i];
-        return k;
-    }
-#endif
-    for (int i = 1; i < kNumKinds; ++i) k += slot >= sc.kind_begin[i];
-    return k;
-}
-
 template <typename R>
 struct Hit {
     R t;
@@ -751,11 +737,8 @@ struct Blocker {
 };
 
 // is_in_shadow (world.rs:98-112): any casting shape with 0 <= t < distance.
-// skip_slot (wave-uniform, -1 = none): a shape the caller knows cannot
-// block any active lane's ray (shade_ray: the shape every lane's point lies
-// on, seen from its outer side).
 template <typename R>
-__device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist, int skip_slot = -1) {
+__device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) {
 #ifdef RTC_ABLATE_SHADOW  // diagnostic builds only (scripts/build_variant.sh -DRTC_ABLATE_...): time without shadow rays
     return false;
 #endif
@@ -766,7 +749,7 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist, 
     // slower in round 3; per cluster cover -2.5 %, cylinders -4 %, table +1 %)
     auto skip = [&](R, R, R, R) { return !wave_any(!b.blocked(dist)); };
     for_all_culled<R, true>(sc, o, d, dd, [&]<int K>(const ShapeRec<R>& s, int slot) {
-        if (!s.casts_shadow || slot == skip_slot) return;  // wave-uniform
+        if (!s.casts_shadow) return;  // wave-uniform
         jit_fence(o, d, slot);
         if (!wave_may_hit<R, K>(s, o, d, dd)) return;
         const V3<R> lo = xform_point(s.inv, o);
@@ -1146,8 +1129,7 @@ __device__ inline void count_events(Counts& k, bool primary, bool hit, const Sha
 template <typename R>
 struct Prepared {
     V3<R> p, n, eye, over, base;
-    int mat;      // the hit's material index
-    bool inside;  // the eye is inside the hit's shape (normal flipped, computed_hit.rs:27-31)
+    int mat;  // the hit's material index
 };
 
 #ifdef RTC_JIT
@@ -1161,8 +1143,7 @@ __device__ inline void prepare_hit_const(const DevScene<float>& sc, V3<float> o,
     asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(w.z));  // the hardware rsq, as hit_normal (bit for bit)
     q.n = normalized(w);
     q.eye = vneg(d);
-    q.inside = dot(q.n, q.eye) < 0.0f;
-    if (q.inside) q.n = vneg(q.n);
+    if (dot(q.n, q.eye) < 0.0f) q.n = vneg(q.n);
     q.mat = -1;  // (the direct kernel walks no refractive indices)
     q.over = along(q.p, q.n, Real<float>::surface_offset(q.p.x, q.p.y, q.p.z));
     q.base = {m.color[0], m.color[1], m.color[2]};
@@ -1187,8 +1168,7 @@ __device__ inline const MaterialRec<R>& prepare_hit(const DevScene<R>& sc, V3<R>
         asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(w.z));  // the hardware rsq, as hit_normal (bit for bit)
         q.n = normalized(w);
         q.eye = vneg(d);
-        q.inside = dot(q.n, q.eye) < (R)0;
-        if (q.inside) q.n = vneg(q.n);
+        if (dot(q.n, q.eye) < (R)0) q.n = vneg(q.n);
         q.mat = mat;
         const MaterialRec<R>& m = sc.lmats[mat];
         q.over = along(q.p, q.n, Real<R>::surface_offset(q.p.x, q.p.y, q.p.z));
@@ -1206,8 +1186,7 @@ __device__ inline const MaterialRec<R>& prepare_hit(const DevScene<R>& sc, V3<R>
     q.p = along(o, d, h.t);
     q.n = hit_normal(s, h.slot, h.kind, q.p);
     q.eye = vneg(d);
-    q.inside = dot(q.n, q.eye) < (R)0;
-    if (q.inside) q.n = vneg(q.n);
+    if (dot(q.n, q.eye) < (R)0) q.n = vneg(q.n);
     q.mat = s.material;
     const MaterialRec<R>& m = sc.lmats[s.material];
     q.over = along(q.p, q.n, Real<R>::surface_offset(q.p.x, q.p.y, q.p.z));
@@ -1291,16 +1270,6 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
 #endif
     const V3<R> p = q.p, n = q.n, eye = q.eye, over = q.over, base = q.base;
     V3<R> surface = {(R)0, (R)0, (R)0};
-    // A shadow ray from the outer side of a convex or flat shape (sphere,
-    // cube; plane, triangle: either side) toward a light on that side (ldn >=
-    // 0) never meets that shape again: the over point lies beyond the plane
-    // that supports the shape at the hit, and the ray moves away from it.  So
-    // when every lane tracing a shadow ray sits on one such shape, the wave
-    // skips that shape's test; the answer is the same (computed_hit.rs:33-34
-    // over point; world.rs:98-112).
-    const int hk = h.kind >= 0 ? h.kind : slot_kind(sc, h.slot);
-    const bool flat = hk == RT_SHAPE_PLANE || hk == RT_SHAPE_TRIANGLE;
-    const int self = (flat || ((hk == RT_SHAPE_SPHERE || hk == RT_SHAPE_CUBE) && !q.inside)) ? h.slot : -1;
     for_lights(sc, [&](const LightRec<R>& L) {
         const V3<R> lpos = {L.position[0], L.position[1], L.position[2]};
         const V3<R> to_light = vsub(lpos, over);
@@ -1313,10 +1282,7 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
         // counters still count one shadow ray per light.
         const R ldn = dot(ld, n);
         bool shadowed = false;
-        if (!(ldn < (R)0)) {
-            const int first = __builtin_amdgcn_readfirstlane(self);  // (over the lanes tracing it)
-            shadowed = any_hit(sc, over, ld, dist, first >= 0 && !wave_any(self != first) ? first : -1);
-        }
+        if (!(ldn < (R)0)) shadowed = any_hit(sc, over, ld, dist);
         const V3<R> c = lighting_term(L, m, base, n, eye, ld, ldn, shadowed);
         surface = {surface.x + c.x, surface.y + c.y, surface.z + c.z};
     });
