@@ -737,8 +737,9 @@ struct Blocker {
 };
 
 // is_in_shadow (world.rs:98-112): any casting shape with 0 <= t < distance.
+// lpos: the light the ray runs to (o + dist d).
 template <typename R>
-__device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) {
+__device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist, V3<R> lpos) {
 #ifdef RTC_ABLATE_SHADOW  // diagnostic builds only (scripts/build_variant.sh -DRTC_ABLATE_...): time without shadow rays
     return false;
 #endif
@@ -753,6 +754,16 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist) 
         jit_fence(o, d, slot);
         if (!wave_may_hit<R, K>(s, o, d, dd)) return;
         const V3<R> lo = xform_point(s.inv, o);
+        if constexpr (K == RT_SHAPE_PLANE) {
+            // A plane blocks the segment from o to the light only if they lie on
+            // opposite sides of it: with both on one side (object y of the same
+            // sign) the crossing, if any, is behind o or beyond the light.  A wave
+            // whose points all share the light's side skips the test.  The ratio
+            // cap keeps the crossing beyond the light by far more than f32
+            // rounding (|y_o| <= 1e4 |y_L|: beyond by a factor >= 1 + 1e-4).
+            const R ly = xform_point(s.inv, lpos).y;
+            if (!wave_any(!(lo.y * ly > (R)0 && Real<R>::fabs(lo.y) <= (R)1e4 * Real<R>::fabs(ly)))) return;
+        }
         const V3<R> ld = xform_vector(s.inv, d);
         entries<R, K>(s, lo, ld, [&](R t, bool v) { b.offer(t, v, dist); });
     }, skip);
@@ -1282,7 +1293,7 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
         // counters still count one shadow ray per light.
         const R ldn = dot(ld, n);
         bool shadowed = false;
-        if (!(ldn < (R)0)) shadowed = any_hit(sc, over, ld, dist);
+        if (!(ldn < (R)0)) shadowed = any_hit(sc, over, ld, dist, lpos);
         const V3<R> c = lighting_term(L, m, base, n, eye, ld, ldn, shadowed);
         surface = {surface.x + c.x, surface.y + c.y, surface.z + c.z};
     });
