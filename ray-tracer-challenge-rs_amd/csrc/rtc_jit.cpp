@@ -203,7 +203,9 @@ Clusters make_clusters(const std::vector<ShapeRec<float>>& sh) {
     // members x radius^2), which k-means cannot see: a large shape pulls its
     // cluster's ball wide (RTC_JIT_CLUSTER_REFINE=0: k-means only)
     const char* rf = std::getenv("RTC_JIT_CLUSTER_REFINE");
-    const bool refine = !(rf && !std::strcmp(rf, "0"));
+    // (quadratic per move: worlds of at most 64 bounded shapes; k-means alone
+    // beyond, which stays O(n k) per iteration)
+    const bool refine = !(rf && !std::strcmp(rf, "0")) && n <= 64;
     auto ball_of = [&](Cl& q) {
         q.cent = {0, 0, 0};
         for (int i : q.m)
