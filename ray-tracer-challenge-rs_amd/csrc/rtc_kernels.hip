@@ -767,7 +767,16 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist, 
                 const R lim_b = (R)1 + (R)1e-5 * ((R)1 + Real<R>::fabs(b));
                 return (a > lim_a && b > lim_b) || (a < -lim_a && b < -lim_b);
             };
-            if (!wave_any(!(out(po.x, pl.x) || out(po.y, pl.y) || out(po.z, pl.z)))) return;
+            bool clear = out(po.x, pl.x) || out(po.y, pl.y) || out(po.z, pl.z);
+            // Nor can a cube that holds the light (1e-4 inside every face) block
+            // a segment starting strictly inside it: every slab's entry is then
+            // at t < 0 and its exit beyond the light (table's room and walls,
+            // each holding the points on the other).  Wave-uniform, and folded
+            // at compile time in the per-scene build.
+            constexpr R kIn = (R)(1 - 1e-4);
+            if (Real<R>::fabs(pl.x) < kIn && Real<R>::fabs(pl.y) < kIn && Real<R>::fabs(pl.z) < kIn)
+                clear = clear || (Real<R>::fabs(po.x) < (R)1 && Real<R>::fabs(po.y) < (R)1 && Real<R>::fabs(po.z) < (R)1);
+            if (!wave_any(!clear)) return;
         }
         if (!wave_may_hit<R, K>(s, o, d, dd)) return;
         const V3<R> lo = xform_point(s.inv, o);
