@@ -48,8 +48,11 @@ for step in "$@"; do
       : > gpurun_out/ab.log
       for r in $(seq ${AB_ROUNDS:-2}); do
         for v in _lib ${AB_VARIANTS:-_lib_acc64}; do
-          for a in "--scene three_sphere_scene" "--scene reflect_refract" "--scene cover --width 3840 --height 2160 --steps 300" \
-                   "--scene table --width 3840 --height 2160 --steps 300"; do
+          # AB_ONLY=direct: three_sphere only (the direct kernel)
+          if [ "${AB_ONLY:-}" = direct ]; then set -- "--scene three_sphere_scene --steps 1000"; else
+            set -- "--scene three_sphere_scene" "--scene reflect_refract" "--scene cover --width 3840 --height 2160 --steps 300" \
+                   "--scene table --width 3840 --height 2160 --steps 300"; fi
+          for a in "$@"; do
             out=$(RTC_LIBRARY=$L/$v/librtc.so timeout -k 10 200 python bench.py $a --no-cpu-baseline --ab 2>>gpurun_out/ab.log | grep '^{')
             rc=$?; [ $rc -eq 0 ] || { echo "ab $v $a rc=$rc"; exit 1; }
             echo "$out" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', d['config']['workload'], 'kernel_ms %.4f' % d['roofline']['kernel_ms'], 'cold', d.get('cold_kernel_ms'), 'jit', d.get('jit_used'))" | tee -a gpurun_out/ab.log
