@@ -91,3 +91,41 @@ def test_cube_shadow_skips_are_exact(dt):
         n_sep += int(clear.sum())
         n_in += int(inside.sum())
     assert n_sep > 10000 and n_in > 1000  # both skips were exercised
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_plane_shadow_side_skip_is_exact(dt):
+    """The plane skip (any_hit, K == plane): the point and the light on the same
+    side of the plane (object y of one sign) with |y_point| <= 1e4 |y_light|.
+    The kernel's plane entry is t = -o.y / d.y (plane.rs:42-48; f32 through the
+    reciprocal), valid for |d.y| >= EPSILON; a skipped lane must have no entry
+    with 0 <= t < distance."""
+    rng = np.random.default_rng(11)
+    n_skip = 0
+    eps = dt(8e-8)
+    for _ in range(200):
+        m, t, inv, tinv = _transform(rng, dt)
+        n = 2000
+        po_true = rng.uniform(-50, 50, (n, 3))
+        pl_true = rng.uniform(-50, 50, (n, 3))
+        near = rng.random(n) < 0.5
+        po_true[near, 1] = rng.choice([1e-6, -1e-6, 1e-3, -1e-3, 1e-5, -1e-5], int(near.sum()))
+        lnear = rng.random(n) < 0.3  # lights just off the plane (the ratio cap's case)
+        pl_true[lnear, 1] = rng.choice([1e-9, -1e-9, 1e-7, -1e-7, 1e-6, -1e-6], int(lnear.sum()))
+        p = (po_true @ m.T + t).astype(dt)
+        light = (pl_true @ m.T + t).astype(dt)
+        v = (light - p).astype(dt)
+        dist = np.sqrt((v * v).sum(axis=1)).astype(dt)
+        ok = dist > 0
+        p, v, dist, light = p[ok], v[ok], dist[ok], light[ok]
+        d = (v / dist[:, None]).astype(dt)
+        oy = (p @ inv.T + tinv).astype(dt)[:, 1]
+        ly = (light @ inv.T + tinv).astype(dt)[:, 1]
+        dy = (d @ inv.T).astype(dt)[:, 1]
+        skip = (oy * ly > 0) & (np.abs(oy) <= dt(1e4) * np.abs(ly))
+        with np.errstate(all="ignore"):
+            tt = (-oy * (dt(1) / dy).astype(dt)).astype(dt)
+        blocked = (np.abs(dy) >= eps) & (tt >= 0) & (tt < dist)
+        assert not (skip & blocked).any(), "plane side test skipped a blocking plane"
+        n_skip += int(skip.sum())
+    assert n_skip > 100000
