@@ -695,6 +695,30 @@ struct Nearest {
 // shape a later entry never displaces an equal t (strict `w < world`), so
 // push order needs no tracking; the loop carries (t, world) only and the
 // slot/kind come from the world_slot table afterwards.
+// Per-scene builds: does this cube hold one of the world's lights (1e-4 inside
+// every face)?  Folded at compile time (constant record and lights): such a
+// cube encloses the scene (table's room and walls), so most rays start inside.
+#ifndef RTC_CUBE_EXIT_PATH
+#define RTC_CUBE_EXIT_PATH 1
+#endif
+template <typename R>
+__device__ inline bool jit_cube_holds_light(const ShapeRec<R>& s) {
+#if defined(RTC_JIT) && RTC_CUBE_EXIT_PATH
+    if constexpr (sizeof(R) == 4) {
+        bool any = false;
+        for (int i = 0; i < jit::kNumLights; ++i) {
+            const V3<R> p = xform_point(s.inv, V3<R>{jit::kLights[i].position[0], jit::kLights[i].position[1],
+                                                     jit::kLights[i].position[2]});
+            constexpr R kIn = (R)(1 - 1e-4);
+            any |= Real<R>::fabs(p.x) < kIn && Real<R>::fabs(p.y) < kIn && Real<R>::fabs(p.z) < kIn;
+        }
+        return any;
+    }
+#endif
+    (void)s;
+    return false;
+}
+
 template <typename R>
 __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
     Nearest<R> best;
@@ -707,6 +731,26 @@ __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
         // (per-scene records: the slot rides below the world index; world
         // indices are distinct, so the order is the world order)
         const int w = kJitRecords && sizeof(R) == 4 ? (s.world_index << 8) | slot : s.world_index;
+        if constexpr (K == RT_SHAPE_CUBE && sizeof(R) == 4) {
+            // A wave whose every origin lies strictly inside an enclosing cube:
+            // each slab's entry is then negative and its exit positive, so the
+            // nearest entry at t >= 0 is the exit, min over the slabs of the
+            // larger bound, which is (+1 - o) r for r > 0 and (-1 - o) r for
+            // r < 0: the same products and fmin order as entries(), without the
+            // entry side.  (t > 0 keeps entries()'s validity bit for bit.)
+            if (jit_cube_holds_light(s) &&
+                !wave_any(!(Real<R>::fabs(lo.x) < (R)1 && Real<R>::fabs(lo.y) < (R)1 && Real<R>::fabs(lo.z) < (R)1))) {
+                using T = Real<R>;
+                auto hi = [](auto org, auto dir) {  // (generic: never formed for f64)
+                    const bool steep = T::fabs(dir) >= T::kEps;
+                    const R r = sel(steep, __builtin_amdgcn_rcpf(dir), T::kMax);
+                    return sel(r > (R)0, (R)1 - org, (R)-1 - org) * r;
+                };
+                const R tmax = T::fmin(T::fmin(T::fmin(T::kMax, hi(lo.x, ld.x)), hi(lo.y, ld.y)), hi(lo.z, ld.z));
+                best.offer(tmax, tmax > (R)0, w);
+                return;
+            }
+        }
         entries<R, K, true>(s, lo, ld, [&](R t, bool v) { best.offer(t, v, w); });
     });
     return best.hit(sc);
