@@ -14,13 +14,14 @@ primary + shadow + reflect + refract).
   renders its own frame per step (independent frames: no data-path
   collective, "scaling": "weak"), so the line's workload per GPU is the same
   at every N and `value` is the whole job's rays / time.
-* With N > 1 the default run then also measures the north star's image-tile
-  split, BASELINE configs[3]: scenes/cover.yaml at 3840x2160, every frame
+* The default run then also measures the north star's image-tile split, at
+  every N (N = 1 included): BASELINE configs[3] and configs[4],
+  scenes/cover.yaml and scenes/table.yaml at 3840x2160, every frame
   split across the N GPUs in cyclic row blocks by librtc's own multi-GPU
   context (csrc/rtc_group.cpp: the scene RCCL-broadcast by rt_scene_upload,
   the strips RCCL-gathered onto rank 0 and de-interleaved there), gathering
   the 8-bit canvas (canvas.rs:117-123; 4x fewer bytes than f32), and attaches
-  it as "tile_split": its Mray/s and ms/frame, per-shard render / gather /
+  them as "tile_split": {"cover": ..., "table": ...}, each with its Mray/s and ms/frame, per-shard render / gather /
   end-to-end milliseconds, and the same frame on rank 0's GPU alone
   (`single_gpu_ms_per_step`, `speedup_vs_1gpu`).  `--mode tiled` makes the
   split the line itself ("scaling": "strong"); `--mode frames` skips it.
@@ -57,7 +58,7 @@ def parse():
                     help="keep warming up (untimed) until at least this much wall time of frames has run, "
                          "whatever --warmup: a few 25 us frames leave the GPU below its steady clocks")
     ap.add_argument("--mode", choices=["auto", "frames", "tiled"], default="auto",
-                    help="auto: a frame per GPU per step, plus (N > 1) the configs[3] tile split as 'tile_split'; "
+                    help="auto: a frame per GPU per step, plus the configs[3]/[4] tile splits as 'tile_split'; "
                          "frames: without it; tiled: the tile split is the line")
     ap.add_argument("--scene", default=None,
                     help="default three_sphere_scene (configs[1]) on one GPU / in frames mode, cover (configs[3]) "
@@ -147,9 +148,11 @@ def cpu_serial_configs0(budget_s):
             "sample": f"{len(times)} frames, f64 C++ restatement of Camera::render on 1 thread, median ms/frame"}
 
 
-def load_traffic(workload: str):
-    """HBM bytes per launch from the committed rocprofv3 --pmc pass (profiles/traffic.json)."""
-    p = os.path.join(ROOT, "profiles", "traffic.json")
+def load_profile(name: str, workload: str):
+    """Per-workload figures from the committed rocprofv3 --pmc passes
+    (scripts/collect_profiles.py): profiles/traffic.json (HBM bytes per
+    launch), profiles/issue.json (VALU issue and wait fractions)."""
+    p = os.path.join(ROOT, "profiles", name)
     try:
         with open(p) as f:
             return json.load(f).get(workload)
@@ -184,7 +187,7 @@ def resolve(args, tiled):
     a = argparse.Namespace(**vars(args))
     if a.scene is None:
         a.scene = "cover" if tiled else "three_sphere_scene"
-    default_4k = tiled and a.scene == "cover"
+    default_4k = tiled and a.scene in SPLIT_SCENES
     a.width = a.width or (3840 if default_4k else 1920)
     a.height = a.height or (2160 if default_4k else 1080)
     a.out = a.out or ("u8" if tiled else "real")
@@ -272,28 +275,43 @@ def main():
     # "tile_split"; --mode tiled makes that split the line itself.
     tiled = args.mode == "tiled"
     line = measure(resolve(args, tiled), tiled, world, rank, local)
-    if world > 1 and args.mode == "auto":
-        split = measure(resolve(args_for_split(args), True), True, world, rank, local)
+    if args.mode == "auto":
+        # The north star's strong-scaling series, at every N (N = 1 included,
+        # so a scaling curve compares one workload): configs[3] and configs[4],
+        # each 4K frame split across the N GPUs by librtc's group context.
+        splits = {}
+        for name in SPLIT_SCENES:
+            split = measure(resolve(args_for_split(args, name), True), True, world, rank, local)
+            if rank == 0:
+                splits[name] = {k: split[k] for k in (
+                    "value", "unit", "ms_per_step", "steps", "scaling", "config", "render_ms_per_shard",
+                    "gather_ms", "frame_ms", "gather", "gather_variants", "single_gpu_ms_per_step",
+                    "speedup_vs_1gpu", "strong_scaling_efficiency", "single_gpu_value", "roofline",
+                    "first_frame_ms") if k in split}
         if rank == 0:
-            line["scaling_note"] = ("value: N independent configs[1] frames per step (weak scaling: a throughput "
-                                    "check, linear by construction); the north star's image-tile split is "
-                                    "tile_split (strong scaling: speedup_vs_1gpu over the same frame on one GPU)")
-            line["tile_split"] = {k: split[k] for k in (
-                "value", "unit", "ms_per_step", "steps", "scaling", "config", "render_ms_per_shard", "gather_ms",
-                "frame_ms", "gather", "gather_variants", "single_gpu_ms_per_step", "speedup_vs_1gpu",
-                "strong_scaling_efficiency", "single_gpu_value", "roofline",
-                "first_frame_ms") if k in split}
+            line["scaling_note"] = (
+                "value: N independent configs[1] frames per step, one per GPU (weak scaling: a throughput check, "
+                "linear by construction) - NOT a scaling result. The north star's image-tile split is tile_split: "
+                "configs[3] (cover) and configs[4] (table) at 3840x2160, each frame split across the N GPUs "
+                "(strong scaling: speedup_vs_1gpu over the same frame on one GPU, at every N)")
+            line["tile_split"] = splits
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def args_for_split(args):
-    """configs[3]'s defaults for the tile-split part of an N > 1 run (the
-    line's own --scene/--width/--height/--out/--depth describe its frames)."""
+# BASELINE configs[3] and configs[4]: the 4K frames the north star splits across GPUs
+SPLIT_SCENES = ("cover", "table")
+
+
+def args_for_split(args, scene):
+    """The tile-split series' workload (configs[3] / configs[4] at 3840x2160,
+    u8 canvas); the line's own --scene/--width/--height/--out/--depth describe
+    its frames."""
     a = argparse.Namespace(**vars(args))
-    a.scene = a.width = a.height = a.out = a.depth = None
+    a.scene = scene
+    a.width = a.height = a.out = a.depth = None
     return a
 
 
@@ -323,7 +341,9 @@ def measure(args, tiled, world, rank, local):
         ctx.set_gather(rtc_amd.RT_GATHER_PEER if args.gather == "peer" else rtc_amd.RT_GATHER_RCCL)
         phase["context_ms"] = (time.perf_counter() - t) * 1e3
         t = time.perf_counter()
-        ctx.upload(scene if rank == 0 else None)
+        # every rank raises if any rank's part of the upload failed (no rank
+        # left waiting in the next collective: rdist.collective_call)
+        rdist.collective_call(lambda: ctx.upload(scene if rank == 0 else None), rank)
         phase["upload_ms"] = (time.perf_counter() - t) * 1e3
         cam0 = rtc_amd.camera_resize(scene.camera, args.width, args.height) if rank == 0 else None
         cam = rdist.share_camera(cam0, rank) if world > 1 else cam0
@@ -474,7 +494,8 @@ def measure(args, tiled, world, rank, local):
         workload = f"{args.scene}@{cam.width}x{cam.height},depth={args.depth},{args.precision}"
         if args.out == "u8":
             workload += ",u8"
-        traffic = load_traffic(workload) if not tiled else None
+        traffic = load_profile("traffic.json", workload) if not tiled else None
+        issue = (load_profile("issue.json", workload) or {}) if not tiled else {}
         line = {
             "metric": "Mray/s (primary+secondary) and ms/frame at 1920x1080",
             "value": total_rays / elapsed / 1e6,
@@ -501,7 +522,11 @@ def measure(args, tiled, world, rank, local):
                          # the north star's HBM view: PMC bytes per launch over the launch time,
                          # against the ~8 TB/s memory roof (a diagnostic: the path is compute-bound)
                          "hbm_gbs": traffic / (kernel_ms * 1e-3) / 1e9 if traffic else None,
-                         "hbm_frac": traffic / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS if traffic else None},
+                         "hbm_frac": traffic / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS if traffic else None,
+                         # the issue side (PMC, same launches): `frac` charges every ray brute force
+                         # over all shapes, so culls count as achieved FLOPs; these
+                         # say how busy the VALU really was and how long waves waited
+                         "valu_issue_frac": issue.get("valu_issue_frac"), "wait_frac": issue.get("wait_frac")},
         }
         if tiled:
             line["roofline"]["kernel"] = "rank 0's shard launch (median of 5 instrumented frames)"
@@ -550,6 +575,18 @@ def measure(args, tiled, world, rank, local):
             d2h_s = (time.perf_counter() - t) / 5
             line["host_frame_floor_ms"] = d2h_s * 1e3
             line["d2h_gbs"] = image.numel() * image.element_size() / d2h_s / 1e9
+            # the same frame as the 8-bit canvas Canvas::to_png_file writes
+            # (RT_OUT_U8: canvas.rs:117-123's quantization on the device, a
+            # quarter of the bytes; INTEGRATION.md 1b'')
+            if args.out != "u8":
+                canvas8, _ = ctx.render(cam, args.depth, args.precision, "u8")
+                lat8 = []
+                for _ in range(10):
+                    t = time.perf_counter()
+                    ctx.render(cam, args.depth, args.precision, "u8", out=canvas8)
+                    lat8.append((time.perf_counter() - t) * 1e3)
+                line["host_frame_u8_ms"] = float(np.median(lat8))
+                line["host_frame_u8_floor_ms"] = d2h_s * 1e3 / image.element_size()
             # rays per generation (each bounce's wavefront size):
             # one untimed diagnostic frame of the generic kernel (RT_FLAG_GENERATIONS)
             _, _, gen = ctx.render_generations(cam, args.depth, args.precision)

@@ -89,18 +89,19 @@ struct rt_context {
     // uniform-cost direct tiles -> static stride; high-variance pool tiles ->
     // per-XCD atomic queues; per-lane stores beat LDS-staged ones (the
     // staging barriers wait for store completion).
-    uint32_t sched_direct = rtc::kSchedStatic;  // RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic
-    uint32_t sched_pool = rtc::kSchedDynamic;
-    bool lds_world = true;      // RTC_LDS_WORLD=0 gathers shade data from global memory
-    bool cull = true;  // RTC_CULL=0 uploads every shape as unbounded (no wave cull; exactness tests)
-    bool kind_variants = true;  // RTC_KIND_VARIANTS=0: always the all-kinds kernels
+    // (RTC_DEBUG=sched_direct=grid|static; the pool kernel always takes the
+    // per-XCD queues)
+    uint32_t sched_direct = rtc::kSchedStatic;
+    bool lds_world = true;      // RTC_DEBUG=lds_world=0 gathers shade data from global memory
+    bool cull = true;  // RTC_DEBUG=cull=0 uploads every shape as unbounded (no wave cull; exactness tests)
+    bool kind_variants = true;  // RTC_DEBUG=kind_variants=0: always the all-kinds kernels
     size_t occ_lds[8] = {};     // occupancy cache: {direct,pool} x {f32,f64} x {global,LDS world}
     int occ_blocks[8] = {};
-    uint32_t pool_lds_rays = 0;  // RTC_POOL_LDS_RAYS: LDS-resident pool slots (0 = sized for occupancy)
+    uint32_t pool_lds_rays = 0;  // RTC_DEBUG=pool_lds_rays=N: LDS-resident pool slots (0 = sized for occupancy)
     void* d_spill = nullptr;     // ray-pool overflow regions, one per resident workgroup
     // Heaviest-first tile order for repeated pool launches of the same frame
     // (order_tiles): per-tile costs of the last launch and its signature.
-    bool tile_order = true;      // RTC_TILE_ORDER=0: raster order always
+    bool tile_order = true;      // RTC_DEBUG=tile_order=0: raster order always
     uint32_t* d_tile_cost = nullptr;
     uint32_t* d_tile_order = nullptr;
     uint32_t order_capacity = 0;
@@ -113,22 +114,22 @@ struct rt_context {
     uint32_t* d_cold_order = nullptr;  // centre-out order + item count, for cold_w x cold_h
     uint32_t cold_w = 0, cold_h = 0;
     // Tiles costing more than split_factor x the mean workgroup load are
-    // handed out in parts (order_tiles); RTC_SPLIT=0 never splits.  Round-3
+    // handed out in parts (order_tiles); RTC_DEBUG=split=0 never splits.  Round-3
     // sweep (per-scene kernels, slowest of 8 shards at 4K / 1-GPU frame):
     // 1.5: cover 0.239 / 1.132 ms, table 0.244 / 1.389; 1.0: 0.217 / 1.142,
     // 0.226 / 1.369; 0.75: 0.206 / 1.128, 0.233 / 1.384; 0.5: 0.205 / 1.128,
     // 0.245 / 1.414; reflect_refract 1080p, slowest of 4: 0.146 / 0.129 /
     // 0.126 / 0.131 with whole frames unchanged (0.385-0.403).
     double split_factor = 1.0;
-    // RTC_SPLIT_MAX: log2 of the most parts a tile is split into.  Same-box
-    // sweep (profiles/r03_split16_sweep.txt, r03_shard_floor.txt), slowest
+    // RTC_DEBUG=split_max=L: log2 of the most parts a tile is split into.  Same-box
+    // sweep (profiles/ab/r03_split16_sweep.txt, r03_shard_floor.txt), slowest
     // shard ms at 2 / 3 / 4: cover 4K of 8 0.198 / 0.202 / 0.207, of 32
     // 0.130 / 0.096 / 0.115; reflect_refract 1080p of 4 0.127 / 0.128 /
     // 0.121, of 16 0.112 / 0.092 / 0.097; whole frames split nothing.
     uint32_t split_max = 3;
     // Items (tiles or parts) costing more than urgent_factor x the mean
     // workgroup load run at raised wave priority, graded 1/2/3 above 1x/2x/4x
-    // that cost (RTC_URGENT, 0 = none; one level for all measured no better).  Same-box sweep, kernel ms, none / flat 0.25 / flat 0.125 /
+    // that cost (RTC_DEBUG=urgent=F, 0 = none; one level for all measured no better).  Same-box sweep, kernel ms, none / flat 0.25 / flat 0.125 /
     // graded 0.125: reflect_refract 0.367 / 0.310 / 0.306 / 0.310, cylinders
     // 0.124 / 0.117 / 0.117 / 0.117, cover 4K 1.014 / 1.023 / 1.011 / 1.011,
     // table 4K, refraction, metal within 1 %; slowest of 8 shards at 4K: cover
@@ -157,10 +158,11 @@ struct rt_context {
     uint32_t jit_pattern_kinds = ~0u;              // pattern kinds in the world's table (bit per RT_PATTERN_*)
     bool jit_transparent = true;                   // some material is transparent (else no refraction code)
     int32_t jit_begin[rtc::kNumKinds + 1] = {};
-    hipFunction_t jit_fn[4] = {};
-    std::shared_ptr<rtc::CodeBuild> jit_build[4];  // the build each variant waits for (host thread)
-    bool jit_rejected[4] = {};   // built, but refused for occupancy or scratch (that variant only)
-    bool jit_owner[4] = {};      // this context started the build: its time goes into jit_compile_ms
+    // variants: pool x LDS world x RT_FLAG_NO_SKIPS (rtc_jit.cpp jit_function)
+    hipFunction_t jit_fn[8] = {};
+    std::shared_ptr<rtc::CodeBuild> jit_build[8];  // the build each variant waits for (host thread)
+    bool jit_rejected[8] = {};   // built, but refused for occupancy or scratch (that variant only)
+    bool jit_owner[8] = {};      // this context started the build: its time goes into jit_compile_ms
     uint32_t jit_frames = 0;     // large f32 frames of this upload so far (RT_JIT_AUTO starts at the 2nd)
     std::string arch;            // the device's gfx target (gcnArchName), for hipRTC; read lazily (device_arch)
     int jit_mode = 2;
@@ -202,7 +204,7 @@ struct rt_context {
 namespace rtc {
 
 // rtc_host.cpp
-// RTC_TRACE_INIT=1: per-step milliseconds of context creation, upload and
+// RTC_DEBUG=trace_init=1: per-step milliseconds of context creation, upload and
 // the first renders on stderr (the one-shot breakdown).
 class InitTrace {
 public:
@@ -231,7 +233,8 @@ int validate_scene(const rt_shape_desc* shapes, uint32_t ns, const rt_material_d
 // Flatten and upload the world tables to this device (no validation, no sync).
 int build_scene(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats, uint32_t nm,
                 const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights, uint32_t nl);
-void scene_brightness(const rt_material_desc* mats, uint32_t nm, const rt_pattern_desc* pats, uint32_t np,
+void scene_brightness(const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats, uint32_t nm,
+                      const rt_pattern_desc* pats, uint32_t np,
                       const rt_light_desc* lights, uint32_t nl, double* bright_hit, double* bright_w);
 // One frame (or shard strip) of this device into `out_device` on `stream`.
 int capture_jit_table(rt_context* ctx);  // the f32 table of the uploaded world, for rtc_jit.cpp
@@ -249,7 +252,8 @@ unsigned long long timeout_ticks(double timeout_ms);
 // rtc_jit.cpp: the per-scene kernel of this context's world for a launch of
 // `static_blocks` workgroups per CU, or null (use the generic kernel)
 constexpr uint32_t kJitMinTiles = 256;  // 64K pixels
-int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int static_blocks, hipFunction_t* fn);
+int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int static_blocks, hipFunction_t* fn,
+                 bool no_skips = false);
 int jit_wait(rt_context* ctx, double timeout_ms, int* pending);
 const std::string& device_arch(rt_context* ctx);  // rtc_jit.cpp: the device's gfx target, read once
 

@@ -278,6 +278,47 @@ int check_group_options(rt_context* ctx, const rt_render_options* o) {
 
 }  // namespace
 
+// The group's agreement on one step's outcome: every member of every rank
+// contributes `local` (RT_OK or its error) to a max all-reduce of -status;
+// RT_ERR_COMM when another rank failed, RT_OK when none did (a member's own
+// failure is returned by its caller).
+int agree_status(const std::vector<rt_context*>& ms, int local) {
+    std::vector<int32_t*> d(ms.size(), nullptr);
+    auto release = [&]() {
+        for (size_t i = 0; i < ms.size(); ++i) {
+            (void)hipSetDevice(ms[i]->device);
+            (void)hipFree(d[i]);
+        }
+    };
+    const int32_t mine = local ? -local : 0;
+    std::vector<int32_t> got(ms.size(), 0);
+    int rc = RT_OK;
+    for (size_t i = 0; i < ms.size() && !rc; ++i) {
+        if (hipSetDevice(ms[i]->device) != hipSuccess || hipMalloc(reinterpret_cast<void**>(&d[i]), sizeof(int32_t)) != hipSuccess ||
+            hipMemcpy(d[i], &mine, sizeof mine, hipMemcpyHostToDevice) != hipSuccess)
+            rc = set_error(RT_ERR_HIP, "status exchange: device buffer");
+    }
+    if (rc) {  // (cannot take part: the other ranks' collective would wait; report it)
+        release();
+        return rc;
+    }
+    ncclResult_t r = ncclGroupStart();
+    for (size_t i = 0; i < ms.size() && r == ncclSuccess; ++i)
+        r = ncclAllReduce(d[i], d[i], 1, ncclInt32, ncclMax, ms[i]->comm, ms[i]->stream);
+    if (r == ncclSuccess) r = ncclGroupEnd();
+    for (size_t i = 0; i < ms.size() && r == ncclSuccess; ++i) {
+        if (hipSetDevice(ms[i]->device) != hipSuccess || hipStreamSynchronize(ms[i]->stream) != hipSuccess ||
+            hipMemcpy(&got[i], d[i], sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+            rc = set_error(RT_ERR_HIP, "status exchange: read back");
+    }
+    release();
+    if (r != ncclSuccess) return set_error(RT_ERR_COMM, std::string("status exchange: ") + ncclGetErrorString(r));
+    if (rc) return rc;
+    for (int32_t g : got)
+        if (g && !local) return set_error(RT_ERR_COMM, "another rank of the group failed (status " + std::to_string(-g) + ")");
+    return RT_OK;
+}
+
 int group_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats,
                        uint32_t nm, const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights,
                        uint32_t nl) {
@@ -343,16 +384,26 @@ int group_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns
     for (const SceneHeader& h : hdr)
         if (h.status) return set_error(h.status, "rt_scene_upload failed on rank 0");
 
-    // 2. the tables, broadcast in place from rank 0's device buffers
+    // 2. the tables, broadcast in place from rank 0's device buffers.  Every
+    // rank first allocates its copies, then the ranks agree on the outcome
+    // (one all-reduce of a status word): a rank whose allocation failed still
+    // takes part, so no other rank is left waiting in the table broadcast.
     std::vector<std::vector<std::pair<void*, size_t>>> bufs(ms.size());
-    for (size_t i = 0; i < ms.size(); ++i) {
+    int local_rc = RT_OK;
+    std::string local_err;
+    for (size_t i = 0; i < ms.size() && !local_rc; ++i) {
         rt_context* m = ms[i];
-        RT_HIP(hipSetDevice(m->device));
-        if (m->rank != 0) {
-            if ((rc = alloc_world(m->w32, hdr[i])) || (rc = alloc_world(m->w64, hdr[i]))) return rc;
+        if (hipSetDevice(m->device) != hipSuccess) local_rc = set_error(RT_ERR_HIP, "hipSetDevice");
+        else if (m->rank != 0) {
+            if ((local_rc = alloc_world(m->w32, hdr[i])) == RT_OK) local_rc = alloc_world(m->w64, hdr[i]);
         }
-        world_buffers(m->w32, hdr[i], bufs[i]);
-        world_buffers(m->w64, hdr[i], bufs[i]);
+        if (local_rc) local_err = rt_last_error();
+    }
+    if ((rc = agree_status(ms, local_rc))) return rc;
+    if (local_rc) return set_error(local_rc, local_err);
+    for (size_t i = 0; i < ms.size(); ++i) {
+        world_buffers(ms[i]->w32, hdr[i], bufs[i]);
+        world_buffers(ms[i]->w64, hdr[i], bufs[i]);
     }
     RT_NCCL(ncclGroupStart());
     for (size_t i = 0; i < ms.size(); ++i)

@@ -23,6 +23,7 @@
 #include "../../include/rtc.h"
 #include "flop_model.hpp"
 #include "host_math.hpp"
+#include "debug_knobs.hpp"
 #include "rtc_context.hpp"
 #include "rtc_internal.hpp"
 #include "shape_identity.hpp"
@@ -43,7 +44,8 @@ hipError_t launch_trace(const LaunchParams<R>& P, bool pool, bool dup, uint32_t 
 constexpr uint32_t kKindsSp = (1u << RT_SHAPE_SPHERE) | (1u << RT_SHAPE_PLANE);
 
 hipError_t launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, uint32_t* n_items, float split_per_cost,
-                              uint32_t max_split_log2, float urgent_per_cost, uint32_t graded, hipStream_t stream);
+                              uint32_t max_split_log2, float urgent_per_cost, uint32_t graded, uint32_t min_split_log2,
+                              hipStream_t stream);
 template <typename R>
 hipError_t launch_debug_shape(const ShapeRec<R>* shapes, int slot, int kind, uint32_t mode, uint32_t world_space,
                               const double* in, uint32_t n, double* out, hipStream_t stream);
@@ -304,12 +306,52 @@ uint32_t tile_rows_for(uint32_t height, uint32_t shards, uint32_t shard) {
     return shard_tile_rows(height, shards, shard);
 }
 
-// Rays held by the LDS pool for a given depth and pop batch (LIFO bound).
-uint32_t pool_capacity(uint32_t depth, uint32_t batch) { return (uint32_t)kBlock + depth * batch; }
+// LIFO bound of a workgroup's ray pool (rays).  Block-lockstep generations
+// pop at most `batch` rays from the top and push at most two children per
+// ray, one level deeper, so the pool never holds more than
+// kBlock + depth x batch.  The free-running variant (-DRTC_POOL_FREE): its
+// four waves each take up to `batch` (64) rays whenever idle and primaries
+// enter lanes only once the LIFO is empty; a simulation of that schedule
+// over random interleavings peaks at 2048 rays for depth 6 and 3648 for
+// depth 10, and 8 x batch x (depth + 1) leaves room above both.  Either way
+// a child past the bound is dropped and flagged (RT_ERR_POOL), never written
+// out of bounds.
+uint32_t pool_capacity(uint32_t depth, uint32_t batch) {
+#ifdef RTC_POOL_FREE
+    return 8 * batch * (depth + 1);
+#else
+    return (uint32_t)kBlock + depth * batch;
+#endif
+}
 
+// Dynamic LDS of the pool (after the world tables): the item slots'
+// accumulators, then `lcap` LIFO slots (a multiple of 8 keeps every array
+// 16-byte aligned).
 template <typename R>
-size_t pool_lds_bytes(uint32_t cap) {
-    return 3 * kBlock * sizeof(PoolAcc<R>) + (size_t)cap * (7 * sizeof(R) + sizeof(PoolMeta));
+size_t pool_lds_bytes(uint32_t lcap) {
+    return (size_t)kTileSlots * 3 * kBlock * sizeof(PoolAcc<R>) + (size_t)lcap * (7 * sizeof(R) + sizeof(PoolMeta));
+}
+
+// Bound on any pixel of the pool kernel: a shaded hit adds at most
+// bright_hit, its children carry at most bright_w of its weight.
+double pixel_bound(double bright_hit, double bright_w, uint32_t depth) {
+    double tree = 0.0, w = 1.0;
+    for (uint32_t g = 0; g <= depth; ++g, w *= bright_w) tree += w;
+    return bright_hit * tree;
+}
+
+// The pool kernel's fixed-point sums hold pixels up to 2^30 x 2^-acc_log2
+// (f32: int32, acc_log2 >= kAccLog2Min) or 2^15 (f64: int64 multiples of
+// 2^-48): a world that may exceed that (a TestPattern on an unbounded
+// surface, or huge light intensities) is refused rather than wrapped.
+int check_pixel_range(const rt_context* ctx, uint32_t depth, bool f32) {
+    const double b = pixel_bound(ctx->bright_hit, ctx->bright_w, depth);
+    const double lim = f32 ? std::ldexp(1.0, 30 - (int)kAccLog2Min) : std::ldexp(1.0, 14);
+    if (!(b < lim))
+        return set_error(RT_ERR_INVALID, "pixel colours of this world are unbounded for the ray pool's fixed-point sums "
+                                         "(bound " + std::to_string(b) + " >= " + std::to_string(lim) +
+                                         "; a TestPattern on an unbounded surface?)");
+    return RT_OK;
 }
 
 // Scale of the f32 pool kernel's int32 pixel sums (rtc_internal.hpp
@@ -320,18 +362,16 @@ size_t pool_lds_bytes(uint32_t cap) {
 // weight (reflectiveness + transparency, world.rs:54-66: Schlick's R and
 // 1 - R are in [0, 1]), so a pixel is below bright_hit x sum_{g<=depth} bright_w^g.
 uint32_t acc_shift_f32(double bright_hit, double bright_w, uint32_t depth) {
-    double tree = 0.0, w = 1.0;
-    for (uint32_t g = 0; g <= depth; ++g, w *= bright_w) tree += w;
-    const double bound = std::max(bright_hit * tree, 1e-30);
+    const double bound = std::max(pixel_bound(bright_hit, bright_w, depth), 1e-30);
     const int s = 30 - (int)std::ceil(std::log2(bound));
     return (uint32_t)std::min<int>(kAccLog2Max, std::max<int>(kAccLog2Min, s));
 }
 
 constexpr size_t kLdsPerCu = 160 * 1024;
-// Static LDS of the tracer kernels (s_tile, s_top: 16 B) plus headroom; the
-// code-object metadata (tests/test_isa_budget.py) checks the real value.
-constexpr size_t kStaticLds = 256;
-constexpr size_t kMaxLds = kLdsPerCu - 8 * 1024;  // dynamic LDS of one workgroup (room for static)
+// Static LDS of the tracer kernels (the pool kernel's per-wave LIFO tops and
+// item tables and the counter flush: 400 B) plus headroom; the code-object
+// metadata (tests/test_isa_budget.py) checks the real value.
+constexpr size_t kStaticLds = 512;
 
 struct LaunchShape {
     int per_cu;  // workgroups per CU the launch is planned for
@@ -364,32 +404,32 @@ int blocks_per_cu(rt_context* ctx, bool pool, bool lds_world, size_t lds, int* p
 }
 
 // LDS-resident part of the ray pool: as many slots as keep the pool kernel
-// at the workgroups/CU its registers allow (4 for f32 at <= 128 VGPRs, vs 2
-// when the whole LIFO bound sat in LDS); the rest of the bound spills to
-// global memory.  RTC_POOL_LDS_RAYS overrides (A/B).
+// at the workgroups/CU its registers allow (6 for f32 at <= 80 VGPRs); the
+// rest of the bound spills to global memory.  RTC_DEBUG=pool_lds_rays=N overrides (A/B).
 template <typename R>
 int pool_lds_rays(rt_context* ctx, uint32_t world_lds, uint32_t cap, uint32_t* lcap) {
+    constexpr uint32_t kMinRays = kBlock;
     if (ctx->pool_lds_rays > 0) {
-        *lcap = std::min<uint32_t>(cap, std::max<uint32_t>(kBlock, ctx->pool_lds_rays));
+        *lcap = std::min<uint32_t>(cap, std::max<uint32_t>(kMinRays, ctx->pool_lds_rays & ~7u));
         return RT_OK;
     }
     const bool lw = world_lds != 0;
     int best = 0, rc;
-    if ((rc = blocks_per_cu<R>(ctx, true, lw, world_lds + pool_lds_bytes<R>(kBlock), &best))) return rc;
+    if ((rc = blocks_per_cu<R>(ctx, true, lw, world_lds + pool_lds_bytes<R>(kMinRays), &best))) return rc;
     if (best < 1) best = 1;
     const size_t rec = 7 * sizeof(R) + sizeof(PoolMeta);
     const size_t budget = (size_t)kLdsPerCu / (size_t)best;
     const size_t fixed = kStaticLds + world_lds + pool_lds_bytes<R>(0) + 511;
-    uint32_t n = budget > fixed ? (uint32_t)((budget - fixed) / rec) : kBlock;
+    uint32_t n = budget > fixed ? (uint32_t)((budget - fixed) / rec) : kMinRays;
     // one workgroup's LDS must also stay within the launch limit
     const size_t room = ctx->lds_per_block > fixed ? ctx->lds_per_block - fixed : 0;
     n = std::min<uint32_t>(n, (uint32_t)(room / rec));
-    n = std::min<uint32_t>(cap, std::max<uint32_t>(kBlock, n & ~31u));
+    n = std::min<uint32_t>(cap, std::max<uint32_t>(kMinRays, n & ~7u));
     for (;;) {  // granule rounding: step down until `best` workgroups fit
         int got = 0;
         if ((rc = blocks_per_cu<R>(ctx, true, lw, world_lds + pool_lds_bytes<R>(n), &got))) return rc;
-        if (got >= best || n <= (uint32_t)kBlock) break;
-        n = std::max<uint32_t>(kBlock, n - 32);
+        if (got >= best || n <= kMinRays) break;
+        n = std::max<uint32_t>(kMinRays, n - 8);
     }
     *lcap = n;
     return RT_OK;
@@ -419,24 +459,13 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
     ls.world_lds = (ctx->lds_world && wb <= kMaxWorldLds && !(jit_records && !ls.pool)) ? (uint32_t)wb : 0;
     ls.lds = ls.world_lds;
     ls.cap = ls.lcap = ls.batch = 0;
-    ls.sched = ls.pool ? ctx->sched_pool : (ctx->sched_direct == kSchedDynamic ? kSchedStatic : ctx->sched_direct);
+    ls.sched = ls.pool ? kSchedDynamic : ctx->sched_direct;
     int rc;
     if (ls.pool) {
-        if (ls.sched == kSchedGrid) {
-            // one workgroup per tile: no per-workgroup spill region, so the
-            // whole LIFO bound lives in LDS (smaller pop batches if needed)
-            const size_t room = std::min(kMaxLds, ctx->lds_per_block - 4096) - ls.world_lds;
-            uint32_t batch = kBlock;
-            while (batch > 32 && pool_lds_bytes<R>(pool_capacity(depth, batch)) > room) batch /= 2;
-            if (pool_lds_bytes<R>(pool_capacity(depth, batch)) > room)
-                return set_error(RT_ERR_INVALID, "max_depth too large for the LDS ray pool");
-            ls.batch = batch;
-            ls.cap = ls.lcap = pool_capacity(depth, batch);
-        } else {
-            ls.batch = kBlock;
-            ls.cap = pool_capacity(depth, kBlock);
-            if ((rc = pool_lds_rays<R>(ctx, ls.world_lds, ls.cap, &ls.lcap))) return rc;
-        }
+        // (the pool kernel takes its items from the per-XCD queues only)
+        ls.batch = kPoolBatch;
+        ls.cap = pool_capacity(depth, ls.batch);
+        if ((rc = pool_lds_rays<R>(ctx, ls.world_lds, ls.cap, &ls.lcap))) return rc;
         ls.lds += pool_lds_bytes<R>(ls.lcap);
     }
     int per_cu = 0;
@@ -493,6 +522,8 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
         ctx->order_capacity = 0;
         ctx->order_valid = ctx->order_built = false;
         RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_tile_cost), P.n_tiles * sizeof(uint32_t)));
+        // (the kernel records a tile's cost as the maximum over its parts)
+        RT_HIP(hipMemsetAsync(ctx->d_tile_cost, 0, P.n_tiles * sizeof(uint32_t), stream));
         // up to 2^kMaxSplitLog2 items per tile, then the item count
         RT_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_tile_order),
                          (((size_t)P.n_tiles << kMaxSplitLog2) + 1) * sizeof(uint32_t)));
@@ -507,7 +538,7 @@ int plan_tile_order(rt_context* ctx, LaunchParams<R>& P, const rt_camera_desc* c
         const float split = ctx->split_factor > 0 ? (float)(ctx->split_factor / grid) : 0.0f;
         const float urgent = ctx->urgent_factor > 0 ? (float)(ctx->urgent_factor / grid) : 0.0f;
         RT_HIP(launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, P.n_tiles, n_items, split, ctx->split_max,
-                                  urgent, 1u, stream));
+                                  urgent, 1u, 0u, stream));
         ++ctx->order_builds;
         ctx->order_built = true;
     }
@@ -621,7 +652,9 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
             if (ctx->lds_world && !ls.pool && w.scene.kind_begin[kNumKinds] <= kJitRecordsMaxShapes &&
                 (rc = plan_launch<R>(ctx, w.scene, depth, P.n_tiles, lj, true)))
                 return rc;
-            if ((rc = jit_function(ctx, lj.pool, lj.world_lds != 0, lj.lds, lj.per_cu, &jf))) return rc;
+            if ((rc = jit_function(ctx, lj.pool, lj.world_lds != 0, lj.lds, lj.per_cu, &jf,
+                                   (flags & RT_FLAG_NO_SKIPS) != 0)))
+                return rc;
             if (jf) ls = lj;
         }
     }
@@ -629,6 +662,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     P.pool_capacity = ls.cap;
     P.pool_lds_capacity = ls.lcap;
     P.pop_batch = ls.batch;
+    if (ls.pool && (rc = check_pixel_range(ctx, depth, sizeof(R) == 4))) return rc;
     P.acc_log2 = acc_shift_f32(ctx->bright_hit, ctx->bright_w, depth);
     if (ls.cap > ls.lcap) {
         const size_t need = (size_t)ls.grid * 8 * (ls.cap - ls.lcap) * sizeof(R);
@@ -651,10 +685,8 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     // previous user of that set is complete by stream order).
     // The set flips only once the launch is enqueued: a launch that fails
     // before that leaves its set unused and still zero for the next one.
-    // (pool launches only: the direct kernel reads no queue heads and zeroes
-    // none, so a dynamic direct launch (RTC_SCHED_DIRECT=dynamic) must not
-    // flip the sets under the next pool launch)
-    const bool dynamic = ls.pool && ls.sched == kSchedDynamic;
+    // (pool launches only: the direct kernel reads no queue heads)
+    const bool dynamic = ls.pool;
     if (dynamic) {
         const size_t set = (size_t)kTileQueues * kQueueStride;
         P.tile_counter = ctx->d_tile_counter + (ctx->head_set ? set : 0);
@@ -691,7 +723,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     // reflect_refract -2.8%, refraction -6.7%.  The direct kernel measured
     // slower that way (three_sphere +2.5%), so it keeps every kind.  Both pool
     // builds are capped at the same waves/SIMD and use the same LDS, so the
-    // occupancy planned above holds.  RTC_KIND_VARIANTS=0 disables.
+    // occupancy planned above holds.  RTC_DEBUG=kind_variants=0 disables.
     uint32_t kinds = 0;
     for (int k = 0; k < kNumKinds; ++k)
         if (w.scene.kind_begin[k + 1] > w.scene.kind_begin[k]) kinds |= 1u << k;
@@ -719,7 +751,7 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     return RT_OK;
 }
 
-InitTrace::InitTrace(const char* what) : what_(what), on_(std::getenv("RTC_TRACE_INIT") != nullptr) {
+InitTrace::InitTrace(const char* what) : what_(what), on_(debug_knob("trace_init", nullptr)) {
     t0_ = t_ = std::chrono::steady_clock::now();
 }
 void InitTrace::step(const char* name) {
@@ -870,7 +902,7 @@ int create_device_context(int device_ordinal, rt_context** out) {
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
         return set_error(RT_ERR_NO_DEVICE, "no HIP device available (the render path has no CPU fallback)");
     if (device_ordinal < 0 || device_ordinal >= n) return set_error(RT_ERR_INVALID, "device ordinal out of range");
-    // RTC_TRACE_INIT=1: milliseconds of each step of context creation on
+    // RTC_DEBUG=trace_init=1: milliseconds of each step of context creation on
     // stderr (the one-shot render's breakdown)
     InitTrace tr("context");
     auto ctx = std::make_unique<rt_context>();
@@ -886,27 +918,24 @@ int create_device_context(int device_ordinal, rt_context** out) {
     tr.step("hipDeviceGetAttribute x2");
     ctx->cu_count = cus;
     ctx->lds_per_block = (size_t)lds;  // launch limit of static + dynamic LDS
-    // scheduling knobs: "grid" (one workgroup per tile, the hardware dispatcher
-    // balances), "static" (resident grid, fixed tile stride) or "dynamic"
-    // (resident grid + per-XCD atomic tile queues)
-    auto sched = [](const char* e, uint32_t dflt) {
-        if (!e) return dflt;
-        if (!std::strcmp(e, "grid")) return kSchedGrid;
-        if (!std::strcmp(e, "static")) return kSchedStatic;
-        if (!std::strcmp(e, "dynamic") || !std::strcmp(e, "persistent")) return kSchedDynamic;
-        return dflt;
-    };
-    ctx->sched_direct = sched(std::getenv("RTC_SCHED_DIRECT"), ctx->sched_direct);
-    ctx->sched_pool = sched(std::getenv("RTC_SCHED_POOL"), ctx->sched_pool);
-    if (const char* e = std::getenv("RTC_LDS_WORLD")) ctx->lds_world = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("RTC_CULL")) ctx->cull = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("RTC_KIND_VARIANTS")) ctx->kind_variants = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("RTC_POOL_LDS_RAYS")) ctx->pool_lds_rays = (uint32_t)std::atoi(e);
-    if (const char* e = std::getenv("RTC_TILE_ORDER")) ctx->tile_order = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("RTC_SPLIT")) ctx->split_factor = std::atof(e);
-    if (const char* e = std::getenv("RTC_SPLIT_MAX"))
-        ctx->split_max = (uint32_t)std::min<int>((int)kMaxSplitLog2, std::max(0, std::atoi(e)));
-    if (const char* e = std::getenv("RTC_URGENT")) ctx->urgent_factor = std::atof(e);
+    // A/B and diagnostic switches (debug_knobs.hpp: RTC_DEBUG=key=value,...)
+    std::string v;
+    // direct-kernel tile scheduling: "grid" (one workgroup per tile, the
+    // hardware dispatcher balances) or "static" (resident grid, fixed stride)
+    if (debug_knob("sched_direct", &v)) {
+        if (v == "grid") ctx->sched_direct = kSchedGrid;
+        else if (v == "static") ctx->sched_direct = kSchedStatic;
+    }
+    if (debug_knob("lds_world", &v)) ctx->lds_world = v != "0";
+    if (debug_knob("cull", &v)) ctx->cull = v != "0";
+    if (debug_knob("kind_variants", &v)) ctx->kind_variants = v != "0";
+    if (debug_knob("pool_lds_rays", &v)) ctx->pool_lds_rays = (uint32_t)std::atoi(v.c_str());
+    if (debug_knob("tile_order", &v)) ctx->tile_order = v != "0";
+    if (debug_knob("split", &v)) ctx->split_factor = std::atof(v.c_str());
+    if (debug_knob("split_max", &v))
+        ctx->split_max = (uint32_t)std::min<int>((int)kMaxSplitLog2, std::max(0, std::atoi(v.c_str())));
+    if (debug_knob("urgent", &v)) ctx->urgent_factor = std::atof(v.c_str());
+    // RTC_JIT: the per-scene build mode (rt_context_set_jit's values), a user setting
     if (const char* e = std::getenv("RTC_JIT"))
         ctx->jit_mode = (e[0] >= '0' && e[0] <= '3' && !e[1]) ? e[0] - '0' : RT_JIT_AUTO;
     RT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
@@ -990,18 +1019,77 @@ int rt_scene_upload(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, c
 
 namespace rtc {
 
-// The brightness bound of acc_shift_f32 for these tables.
-void scene_brightness(const rt_material_desc* mats, uint32_t nm, const rt_pattern_desc* pats, uint32_t np,
-                      const rt_light_desc* lights, uint32_t nl, double* bright_hit, double* bright_w) {
-    double pat = 0.0;  // any pattern colour a material may show (complex sub-patterns included)
-    for (uint32_t i = 0; i < np; ++i)
-        for (int c = 0; c < 3; ++c) pat = std::max({pat, std::fabs(pats[i].color_a[c]), std::fabs(pats[i].color_b[c])});
+// Largest |coordinate| of a point of the shape's surface in object space
+// (+inf for an unbounded surface): the reach of a TestPattern on it.
+double object_extent(const rt_shape_desc& d) {
+    const double inf = std::numeric_limits<double>::infinity();
+    switch (d.kind) {
+        case RT_SHAPE_SPHERE:
+        case RT_SHAPE_CUBE: return 1.0;
+        case RT_SHAPE_CYLINDER:
+            return std::isfinite(d.minimum) && std::isfinite(d.maximum)
+                       ? std::max({1.0, std::fabs(d.minimum), std::fabs(d.maximum)})
+                       : inf;
+        case RT_SHAPE_CONE:
+            return std::isfinite(d.minimum) && std::isfinite(d.maximum)
+                       ? std::max(std::fabs(d.minimum), std::fabs(d.maximum))
+                       : inf;
+        case RT_SHAPE_TRIANGLE: {
+            double e = 0.0;
+            for (int k = 0; k < 3; ++k)
+                e = std::max({e, std::fabs(d.vertex_1[k]), std::fabs(d.vertex_1[k] + d.edge_1[k]),
+                              std::fabs(d.vertex_1[k] + d.edge_2[k])});
+            return e;
+        }
+        default: return inf;  // plane
+    }
+}
+
+// The brightness bound of acc_shift_f32 for these tables: the largest
+// colour a material can show (its colour, the colours of every pattern its
+// pattern reaches, and for a TestPattern, pattern.rs:55-58, the pattern-space
+// point itself: bounded by the surface's object-space extent through the
+// material's pattern transform, +inf on an unbounded surface), times the
+// lights' intensities and the Phong coefficients.
+void scene_brightness(const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats, uint32_t nm,
+                      const rt_pattern_desc* pats, uint32_t np, const rt_light_desc* lights, uint32_t nl,
+                      double* bright_hit, double* bright_w) {
+    // per material: the colours its pattern chain may return, and whether a
+    // TestPattern is among them
+    std::vector<double> col(nm, 0.0);
+    std::vector<char> test(nm, 0);
+    for (uint32_t i = 0; i < nm; ++i) {
+        for (int c = 0; c < 3; ++c) col[i] = std::max(col[i], std::fabs(mats[i].color[c]));
+        std::vector<int32_t> todo;
+        std::vector<char> seen(np, 0);
+        if (mats[i].pattern >= 0 && (uint32_t)mats[i].pattern < np) todo.push_back(mats[i].pattern);
+        while (!todo.empty()) {
+            const int32_t q = todo.back();
+            todo.pop_back();
+            if (q < 0 || (uint32_t)q >= np || seen[q]) continue;
+            seen[q] = 1;
+            const rt_pattern_desc& pd = pats[q];
+            if (pd.kind == RT_PATTERN_TEST) test[i] = 1;
+            else if (pd.kind == RT_PATTERN_COMPLEX) todo.insert(todo.end(), {pd.sub_a, pd.sub_b});
+            else
+                for (int c = 0; c < 3; ++c) col[i] = std::max({col[i], std::fabs(pd.color_a[c]), std::fabs(pd.color_b[c])});
+        }
+    }
+    for (uint32_t s = 0; s < ns; ++s) {  // a TestPattern's colour: the pattern-space point
+        const int32_t m = shapes[s].material;
+        if (m < 0 || (uint32_t)m >= nm || !test[m]) continue;
+        const double ext = object_extent(shapes[s]) * (1.0 + 1e-3) + 1e-3;  // (over_point: a hair off the surface)
+        const double* inv = pats[mats[m].pattern].inverse;  // (a complex pattern's subs use its transform)
+        for (int r = 0; r < 3; ++r) {
+            const double v = (std::fabs(inv[4 * r]) + std::fabs(inv[4 * r + 1]) + std::fabs(inv[4 * r + 2])) * ext +
+                             std::fabs(inv[4 * r + 3]);
+            col[m] = std::max(col[m], std::isnan(v) ? std::numeric_limits<double>::infinity() : v);
+        }
+    }
     double per_light = 0.0, w = 0.0;
     for (uint32_t i = 0; i < nm; ++i) {
         const rt_material_desc& m = mats[i];
-        double c = m.pattern >= 0 ? pat : 0.0;
-        for (int k = 0; k < 3; ++k) c = std::max(c, std::fabs(m.color[k]));
-        per_light = std::max(per_light, c * (std::fabs(m.ambient) + std::fabs(m.diffuse)) + std::fabs(m.specular));
+        per_light = std::max(per_light, col[i] * (std::fabs(m.ambient) + std::fabs(m.diffuse)) + std::fabs(m.specular));
         w = std::max(w, std::fabs(m.reflectiveness) + std::fabs(m.transparency));
     }
     double hit = 0.0;
@@ -1010,8 +1098,8 @@ void scene_brightness(const rt_material_desc* mats, uint32_t nm, const rt_patter
         for (int k = 0; k < 3; ++k) in = std::max(in, std::fabs(lights[l].intensity[k]));
         hit += in * per_light;
     }
-    *bright_hit = std::isfinite(hit) ? hit : 1e300;
-    *bright_w = std::isfinite(w) ? w : 1e300;
+    *bright_hit = std::isfinite(hit) ? hit : std::numeric_limits<double>::infinity();
+    *bright_w = std::isfinite(w) ? w : std::numeric_limits<double>::infinity();
 }
 
 int build_scene(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const rt_material_desc* mats, uint32_t nm,
@@ -1029,7 +1117,7 @@ int build_scene(rt_context* ctx, const rt_shape_desc* shapes, uint32_t ns, const
         ctx->flops.per_ray += shape_test_flops(d.kind, d.closed != 0);
     }
     ctx->flops.n_lights = nl;
-    scene_brightness(mats, nm, pats, np, lights, nl, &ctx->bright_hit, &ctx->bright_w);
+    scene_brightness(shapes, ns, mats, nm, pats, np, lights, nl, &ctx->bright_hit, &ctx->bright_w);
     ctx->have_scene = true;
     ++ctx->scene_gen;  // invalidates the recorded tile costs
     return RT_OK;
@@ -1063,7 +1151,7 @@ int capture_jit_table(rt_context* ctx) {
     ctx->jit_pattern_kinds = 0;
     for (const PatternRec<float>& q : ctx->jit_pattern_recs)  // every kind a pattern_color walk can meet (complex sub-patterns included)
         ctx->jit_pattern_kinds |= 1u << std::min<uint32_t>((uint32_t)q.kind, RT_PATTERN_TEST);
-    for (int v = 0; v < 4; ++v) {
+    for (int v = 0; v < 8; ++v) {
         ctx->jit_fn[v] = nullptr;
         ctx->jit_build[v].reset();
         ctx->jit_rejected[v] = ctx->jit_owner[v] = false;

@@ -52,6 +52,20 @@ RTC_HD inline void shard_of_image_row(uint32_t y, uint32_t shards, uint32_t* sha
 }
 
 constexpr int kBlock = 256;        // threads per workgroup = 4 waves of 64
+constexpr int kWaves = kBlock / 64;  // waves per workgroup
+// The pool kernel's shape (rtc_kernels.hip trace_pool): the default build
+// runs block-lockstep generations of up to kBlock rays over one tile's pixel
+// accumulators; the free-running variant (-DRTC_POOL_FREE) lets each wave
+// take up to 64 rays at a time and holds kTileSlots items (each with its own
+// accumulators; a ray's pool meta carries its item's slot).
+#ifdef RTC_POOL_FREE
+constexpr int kTileSlots = 2;
+static_assert(kTileSlots == 2, "the pool meta carries one slot bit (pixel | slot << 8 | remaining << 9)");
+constexpr uint32_t kPoolBatch = 64;  // rays a wave takes at once
+#else
+constexpr int kTileSlots = 1;
+constexpr uint32_t kPoolBatch = kBlock;  // rays a generation pops
+#endif
 constexpr int kTilePixels = RT_TILE_W * RT_TILE_H;  // one tile per workgroup pass
 static_assert(kTilePixels == kBlock, "one pixel per thread per tile");
 constexpr int kNumKinds = 6;
@@ -71,18 +85,18 @@ constexpr int kTileQueues = 8;
 // cache line, so every XCD's dequeues serialized on it (~17 us per 1792
 // dequeues on MI355X).
 constexpr int kQueueStride = 32;
-// Work items of a cost-ordered pool launch: a tile, or one part of a tile
-// split 2, 4, 8 or 16 ways (order_tiles).  item = tile | part << 20 |
-// log2(parts) << 24 | priority << 27; part p of a tile split 2^l ways seeds
-// the pixels of threads t with t >> (8 - l) == p (halves, wave pairs, waves,
-// half-waves, wave rows).  Cost-ordered launches need n_tiles <= 2^20
+// Work items of a cost-ordered pool launch: one part of a tile split 4 to 64
+// ways (order_tiles).  item = tile | part << 20 | log2(parts) << 26 |
+// priority << 29; part p of a tile split 2^l ways seeds the pixels of
+// threads t with t >> (8 - l) == p (waves, half-waves, wave rows, half rows
+// and quarter rows of a wave's 16 x 4 block).  Cost-ordered launches need n_tiles <= 2^20
 // (plan_tile_order; larger frames keep raster order).
 // An item of priority p > 0 (the costliest, order_tiles) runs its waves at
 // s_setprio(p).
 constexpr uint32_t kItemTileMask = 0xFFFFFu;
-constexpr uint32_t kItemPartShift = 20, kItemSplitShift = 24, kItemPartMask = 15u, kItemSplitMask = 7u;
-constexpr uint32_t kItemPrioShift = 27;
-constexpr uint32_t kMaxSplitLog2 = 4;  // up to 16 items per tile
+constexpr uint32_t kItemPartShift = 20, kItemSplitShift = 26, kItemPartMask = 63u, kItemSplitMask = 7u;
+constexpr uint32_t kItemPrioShift = 29;  // (bit 31 stays clear: no item equals kNoItem)
+constexpr uint32_t kMaxSplitLog2 = 6;  // up to 64 items per tile (4 pixels each)
 // order_tiles runs on launches 2 .. 1 + kOrderBuilds of a frame signature,
 // then the order is reused (rtc_host.cpp plan_tile_order).
 constexpr int kOrderBuilds = 8;
@@ -148,7 +162,7 @@ RTC_HD inline uint32_t div_by(uint32_t t, uint32_t d, uint32_t magic) {
 RTC_HD inline uint64_t canvas_flag_offset(uint64_t image_bytes) {
     return (image_bytes + kCanvasFlagAlign - 1) / kCanvasFlagAlign * kCanvasFlagAlign;
 }
-// Tile scheduling modes (RTC_SCHED_DIRECT / RTC_SCHED_POOL = grid|static|dynamic)
+// Tile scheduling modes (the direct kernel: RTC_DEBUG=sched_direct=grid|static; the pool kernel: dynamic)
 constexpr uint32_t kSchedGrid = 0;     // one workgroup per tile; the dispatcher balances
 constexpr uint32_t kSchedDynamic = 1;  // resident grid, per-XCD atomic tile queues
 constexpr uint32_t kSchedStatic = 2;   // resident grid, tiles b, b+G, ... (no atomics)
@@ -182,7 +196,7 @@ template <typename R>
 using PoolAcc = long long;
 #endif
 constexpr uint32_t kAccLog2Min = 8, kAccLog2Max = 28;
-// A pool entry's meta word (pixel | remaining << 8: 8 + 5 bits) as stored in
+// A pool entry's meta word (pixel | slot << 8 | remaining << 9: 14 bits) as stored in
 // the LDS part of the pool; spilled entries keep 32 bits in their record.
 #ifndef RTC_POOL_META32  // (A/B builds: -DRTC_POOL_META32 keeps 32-bit entries)
 using PoolMeta = uint16_t;
@@ -278,6 +292,7 @@ struct DevScene {
     int32_t n_materials, n_patterns;
     int32_t n_lights;
     int32_t any_secondary;  // some material has reflectiveness or transparency != 0
+    int32_t no_skips;       // RT_FLAG_NO_SKIPS launch (the generic kernels; per-scene builds: RTC_NO_SKIPS)
 };
 
 // One launch of the tracer.
@@ -299,7 +314,7 @@ struct LaunchParams {
     uint32_t max_depth;      // `remaining` of the primary ray
     uint32_t pool_capacity;  // pool kernel: LIFO bound (rays) per workgroup
     uint32_t pool_lds_capacity;  // of which held in LDS; the rest in `spill`
-    uint32_t pop_batch;      // pool kernel: rays popped per iteration (<= kBlock)
+    uint32_t pop_batch;      // pool kernel: rays a wave traces per iteration (<= 64)
     uint32_t acc_log2;       // f32 pool kernel: pixel sums in int32 multiples of 2^-acc_log2
     uint32_t persistent;     // kSched*: tile scheduling of this launch
     uint32_t flags;          // RT_FLAG_* diagnostic ablations

@@ -56,6 +56,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include "debug_knobs.hpp"
 #include "rtc_context.hpp"
 #include "rtc_jit_cache.hpp"
 #include "rtc_jit_sources.inc"  // kSrcKernels, kSrcInternal, kSrcRtcH, kBuildExtra (tools/embed_sources.py)
@@ -105,7 +106,7 @@ std::string ball4(const float* a) {  // a cluster ball: 4 floats
 // centres (farthest-point seeds: deterministic; k from 2 to 8 by the cost
 // model below), each cluster's ball enclosing its members' padded balls.
 // Worlds of fewer than kClusterMinShapes bounded shapes get none
-// (RTC_JIT_CLUSTERS=0: never; =k: k clusters, for sweeps; =1: one cluster of
+// (RTC_DEBUG=jit_clusters=0: never; =k: k clusters, for sweeps; =1: one cluster of
 // every bounded shape, from two shapes on).
 constexpr int kClusterMinShapes = 6;
 struct Clusters {
@@ -120,7 +121,8 @@ Clusters make_clusters(const std::vector<ShapeRec<float>>& sh) {
         if (std::isfinite(r2) && r2 >= 0.0f) bounded.push_back(i);
         else c.unclustered.push_back(i);
     }
-    const char* e = std::getenv("RTC_JIT_CLUSTERS");
+    std::string knob;  // RTC_DEBUG=jit_clusters=N
+    const char* e = debug_knob("jit_clusters", &knob) ? knob.c_str() : nullptr;
     const int n = (int)bounded.size();
     auto flat = [&]() {
         c.unclustered.insert(c.unclustered.end(), bounded.begin(), bounded.end());
@@ -201,8 +203,9 @@ Clusters make_clusters(const std::vector<ShapeRec<float>>& sh) {
     // k-means groups by centre only; a local search then moves single shapes
     // between clusters while that lowers the model's cost (sum over clusters of
     // members x radius^2), which k-means cannot see: a large shape pulls its
-    // cluster's ball wide (RTC_JIT_CLUSTER_REFINE=0: k-means only)
-    const char* rf = std::getenv("RTC_JIT_CLUSTER_REFINE");
+    // cluster's ball wide (RTC_DEBUG=jit_cluster_refine=0: k-means only)
+    std::string rknob;  // RTC_DEBUG=jit_cluster_refine=0
+    const char* rf = debug_knob("jit_cluster_refine", &rknob) ? rknob.c_str() : nullptr;
     // (quadratic per move: worlds of at most 64 bounded shapes; k-means alone
     // beyond, which stays O(n k) per iteration)
     const bool refine = !(rf && !std::strcmp(rf, "0")) && n <= 64;
@@ -380,7 +383,8 @@ std::vector<std::string> build_defines() {
 }
 
 // Everything the compiler sees for one build, and the key naming it.
-jitfile::Request make_request(const std::string& scene, const char* name, const std::string& arch, uint64_t* key) {
+jitfile::Request make_request(const std::string& scene, const char* name, const std::string& arch, uint64_t* key,
+                              bool no_skips) {
     jitfile::Request rq;
     rq.name = name;
     rq.main_src = std::string("#define RTC_JIT 1\n#include \"rtc_jit_scene.hpp\"\n") + kSrcKernels;
@@ -404,15 +408,16 @@ jitfile::Request make_request(const std::string& scene, const char* name, const 
     // -3.6 %, three_sphere 4K -2.5 %, 1080p -0.6 %; the pool kernel lost 15 %
     // on cover that way and keeps a fence per shape.
     if (!std::strstr(name, "pool")) rq.opts.push_back("-DRTC_JIT_FENCE_EVERY=3");
+    // RT_FLAG_NO_SKIPS launches (exactness tests) run a build without the skips
+    if (no_skips) rq.opts.push_back("-DRTC_NO_SKIPS");
     // Shape records as constants (rtc_kernels.hip kJitRecords) pay off in the
-    // direct kernel only.  Same-box A/B, two rounds (profiles/r04_ab_builds.log):
+    // direct kernel only.  Same-box A/B, two rounds (profiles/ab/r04_ab_builds.log):
     // direct three_sphere 17.0 us with them vs 18.4 us without; pool kernels
     // without them reflect_refract -3.0 %, table -1.2 %, cover -0.6 % (the
     // per-slot branches cost more than the extra LDS pool slots gain).
     else rq.opts.push_back("-DRTC_JIT_NO_RECORDS");
-    // RTC_JIT_FLAGS: extra compiler options, space- or comma-separated (A/B diagnostics)
-    if (const char* e = std::getenv("RTC_JIT_FLAGS")) {
-        const std::string all(e);
+    // RTC_DEBUG=jit_flags=...: extra compiler options, space-separated (A/B diagnostics)
+    if (std::string all; debug_knob("jit_flags", &all)) {
         for (size_t p = 0; p < all.size();) {
             size_t q = all.find_first_of(" ,", p);
             if (q == std::string::npos) q = all.size();
@@ -577,10 +582,11 @@ const std::string& device_arch(rt_context* ctx) {
 // generic kernel this launch).  RT_JIT_SYNC builds in line; RT_JIT_AUTO /
 // RT_JIT_EAGER start the build at the 2nd / 1st large frame of an upload and
 // return null until it has landed.
-int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int static_blocks, hipFunction_t* fn) {
+int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int static_blocks, hipFunction_t* fn,
+                 bool no_skips) {
     *fn = nullptr;
     if (ctx->jit_failed || ctx->jit_shapes.empty()) return RT_OK;
-    const int variant = (pool ? 2 : 0) + (lds ? 1 : 0);
+    const int variant = (no_skips ? 4 : 0) + (pool ? 2 : 0) + (lds ? 1 : 0);
     if (ctx->jit_fn[variant]) {
         *fn = ctx->jit_fn[variant];
         return RT_OK;
@@ -620,7 +626,7 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
                 make_request(scene_header(ctx->jit_shapes, ctx->jit_begin, ctx->jit_lights, ctx->jit_materials,
                                           ctx->jit_patterns,
                                           ctx->jit_pattern_kinds, ctx->jit_transparent),
-                             kernel_name(pool, lds), device_arch(ctx), &key);
+                             kernel_name(pool, lds), device_arch(ctx), &key, no_skips);
             start_build(b, rq, key, sync);
         }
     }

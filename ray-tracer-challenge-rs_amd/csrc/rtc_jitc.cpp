@@ -20,6 +20,7 @@
 #include <string>
 #include <vector>
 
+#include "debug_knobs.hpp"
 #include "rtc_jit_cache.hpp"
 
 using namespace rtc::jitfile;
@@ -78,7 +79,7 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "rtc_jitc: cannot write %s\n", argv[2]);
         return 1;
     }
-    if (const char* dir = std::getenv("RTC_JIT_DUMP")) {  // diagnostics: scene header + code object
+    if (std::string dir; rtc::debug_knob("jit_dump", &dir)) {  // diagnostics: scene header + code object
         const std::string base = std::string(dir) + "/" +
                                  std::to_string(fnv(rq.headers.empty() ? "" : rq.headers[0].second.data(),
                                                     rq.headers.empty() ? 0 : rq.headers[0].second.size())) +

@@ -37,6 +37,8 @@ RT_DEFAULT_MAX_DEPTH = 6  # World::MAX_REFLECTION_ITERATIONS, world.rs:15
 RT_MAX_SUPPORTED_DEPTH = 16
 
 RT_OK = 0
+RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NO_DEVICE, RT_ERR_NO_SCENE = -1, -2, -3, -4
+RT_ERR_OOM, RT_ERR_POOL, RT_ERR_IO, RT_ERR_COMM = -5, -6, -7, -8
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_HIP", -3: "RT_ERR_NO_DEVICE", -4: "RT_ERR_NO_SCENE",
           -5: "RT_ERR_OOM", -6: "RT_ERR_POOL", -7: "RT_ERR_IO", -8: "RT_ERR_COMM"}
 RT_UNIQUE_ID_BYTES = 128
@@ -49,6 +51,7 @@ PRECISIONS = {"f32": 0, "f64": 1}
 # rt_render_options.flags: diagnostic ablations (rtc.h); never in a parity or bench result
 RT_FLAG_NO_COUNTERS, RT_FLAG_NO_SHADE, RT_FLAG_NO_TRACE, RT_FLAG_STAMPS, RT_FLAG_FAIL_LAUNCH = 1, 2, 4, 8, 16
 RT_FLAG_GENERATIONS = 32  # count rays per generation (rt_read_generation_counts); pixels unchanged
+RT_FLAG_NO_SKIPS = 64  # no shadow-ray skips or cube exit path (acceleration only: pixels and counters unchanged)
 RT_JIT_OFF, RT_JIT_SYNC, RT_JIT_AUTO, RT_JIT_EAGER = 0, 1, 2, 3
 OUT_FORMATS = {"real": 0, "u8": 1}
 
@@ -468,10 +471,10 @@ class Context:
         return RenderOptions(depth, PRECISIONS[precision], OUT_FORMATS[out_format], shard[0], shard[1], flags)
 
     def render(self, camera: CameraDesc, depth: int = RT_DEFAULT_MAX_DEPTH, precision: str = "f32",
-               out_format: str = "real", shard=(0, 1), out: np.ndarray | None = None):
+               out_format: str = "real", shard=(0, 1), out: np.ndarray | None = None, flags: int = 0):
         """Render one frame (or one shard's strip) into a host array (H, W, 3); returns (image, stats).
         `out` reuses a caller's array of that shape and dtype (a canvas kept across frames)."""
-        opts = self.options(depth, precision, out_format, shard)
+        opts = self.options(depth, precision, out_format, shard, flags)
         rows = camera.height if shard[1] == 1 else shard_rows(camera.height, shard[1])
         dtype = np.uint8 if out_format == "u8" else (np.float32 if precision == "f32" else np.float64)
         if out is not None:

@@ -153,3 +153,39 @@ def share_camera(camera, rank: int, src: int = 0):
     box = [bytes(camera) if rank == src else None]
     dist.broadcast_object_list(box, src=src)
     return CameraDesc.from_buffer_copy(box[0])
+
+
+def collective_call(fn, rank: int, device="cpu"):
+    """Run one rank's part of a collective librtc step (fn() on this rank)
+    and agree on its outcome before anyone goes on: every rank contributes
+    its status (0, or the RenderError code it raised) to one all-reduce, and
+    if any rank failed, every rank raises (the failing ones their own error,
+    the others RT_ERR_COMM naming the first failing rank).  So a rank that
+    fails its upload cannot leave the others waiting in the next collective
+    (bench.py's tiled mode; the library's own group upload agrees the same
+    way over RCCL, rtc_group.cpp)."""
+    import torch
+    import torch.distributed as dist
+
+    from . import RT_ERR_COMM, RenderError
+    err, result = None, None
+    try:
+        result = fn()
+    except RenderError as e:
+        err = e
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        if err is not None:
+            raise err
+        return result
+    world = dist.get_world_size()
+    # per rank: 0 = ok, else -code (codes are negative): one MAX reduce of a world-long vector
+    st = torch.zeros(world, dtype=torch.int64, device=device)
+    st[rank] = 0 if err is None else max(1, -int(err.code))
+    dist.all_reduce(st, op=dist.ReduceOp.MAX)
+    if err is not None:
+        raise err
+    bad = [r for r in range(world) if int(st[r]) != 0]
+    if bad:
+        raise RenderError(RT_ERR_COMM, f"rank {bad[0]} failed this step (status {-int(st[bad[0]])}); "
+                                       f"failed ranks: {bad}")
+    return result

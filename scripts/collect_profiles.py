@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
 """Copy a round's rocprofv3 results from gpurun_out/ into profiles/ (tracked):
-kernel-trace stats CSVs, per-dispatch PMC averages, and profiles/traffic.json —
+kernel-trace stats CSVs, per-dispatch PMC averages, profiles/traffic.json —
 HBM bytes per launch keyed by bench workload, computed as the guide prescribes
 (MI355X_MICROARCH.md "HBM": FETCH_SIZE/WRITE_SIZE are KiB; gfx950 FETCH_SIZE
-counts half of a wide streamed read, so it is doubled).
+counts half of a wide streamed read, so it is doubled) — and profiles/issue.json:
+the issue side of the same launches, beside the roofline's brute-force FLOP
+fraction (which credits every cull as achieved work):
+  valu_issue_frac = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x kernel cycles at 2.4 GHz)
+  wait_frac       = SQ_WAIT_ANY / SQ_WAVE_CYCLES
 
 Usage: python scripts/collect_profiles.py r02
 """
@@ -55,6 +59,8 @@ def main():
     os.makedirs(out, exist_ok=True)
     tp = os.path.join(out, "traffic.json")
     traffic = json.load(open(tp)) if os.path.exists(tp) else {}
+    ip = os.path.join(out, "issue.json")
+    issue = json.load(open(ip)) if os.path.exists(ip) else {}
     for key, workload in SCENES.items():
         src = os.path.join(ROOT, "gpurun_out", f"{rnd}_stats_{key}")
         for f in glob.glob(os.path.join(src, "**", "*kernel_stats.csv"), recursive=True):
@@ -74,9 +80,18 @@ def main():
             hbm = (2 * m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024
             m["hbm_bytes_per_launch"] = hbm
             traffic[workload] = hbm
+        tracer = [v for k, v in med.items() if "trace_" in k]
+        if tracer and "SQ_INSTS_VALU" in m and "SQ_WAVE_CYCLES" in m and "SQ_WAIT_ANY" in m:
+            k_us = max(tracer, key=lambda v: v["calls"])["median_us"]  # the bench's kernel
+            cycles = k_us * 1e-6 * 2.4e9
+            m["valu_issue_frac"] = m["SQ_INSTS_VALU"] * 2 / (1024 * cycles)
+            m["wait_frac"] = m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"]
+            issue[workload] = {"valu_issue_frac": m["valu_issue_frac"], "wait_frac": m["wait_frac"],
+                               "kernel_us": k_us, "source": f"profiles/{rnd}_pmc_{key}.json"}
         json.dump(m, open(os.path.join(out, f"{rnd}_pmc_{key}.json"), "w"), indent=1)
         print(key, json.dumps(m))
     json.dump(traffic, open(tp, "w"), indent=1)
+    json.dump(issue, open(ip, "w"), indent=1)
 
 
 if __name__ == "__main__":

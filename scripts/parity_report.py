@@ -5,6 +5,7 @@ pixel agreement after 8-bit quantization (canvas.rs:117-123), mean/max |err|
 and ray-counter deltas.  The numbers back DESIGN.md's tolerance statement.
 
 Usage: python scripts/parity_report.py [--sizes 160x120,320x240] [--out gpurun_out/parity.json]
+       python scripts/parity_report.py --configs   (BASELINE configs[0]-[4] at their own sizes)
 """
 import argparse
 import json
@@ -26,6 +27,9 @@ def main():
     ap.add_argument("--scenes", default=",".join(SCENES))
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "parity.json"))
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--configs", action="store_true",
+                    help="BASELINE.json configs[0]-[4]: three_sphere 320x240 and 1920x1080, reflect_refract "
+                         "1920x1080, cover and table 3840x2160 (each scene at its own size only)")
     args = ap.parse_args()
     import numpy as np
 
@@ -35,10 +39,15 @@ def main():
 
     rows = []
     ctx = rtc_amd.Context(0)
-    for name in args.scenes.split(","):
+    if args.configs:
+        work = [("three_sphere_scene", ["320x240", "1920x1080"]), ("reflect_refract", ["1920x1080"]),
+                ("cover", ["3840x2160"]), ("table", ["3840x2160"])]
+    else:
+        work = [(name, args.sizes.split(",")) for name in args.scenes.split(",")]
+    for name, sizes in work:
         scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{name}.json"))
         ctx.upload(scene)
-        for size in args.sizes.split(","):
+        for size in sizes:
             w, h = map(int, size.split("x"))
             cam = rtc_amd.camera_resize(scene.camera, w, h)
             t0 = time.time()
@@ -57,6 +66,9 @@ def main():
                        "rays_gpu": int(st["rays"]), "rays_oracle": int(rst["rays"]),
                        "counters_equal": all(st[k] == rst[k] for k in ("primary", "shadow", "reflect", "refract",
                                                                           "shaded")),
+                       # per ray kind: (gpu - oracle) / oracle (0 when the oracle has none)
+                       "kind_rel_delta": {k: (st[k] - rst[k]) / rst[k] if rst[k] else float(st[k] != 0)
+                                          for k in ("primary", "shadow", "reflect", "refract", "shaded")},
                        "kernel_ms": st["kernel_ms"], "oracle_s": t_cpu}
                 rows.append(row)
                 print(json.dumps(row), flush=True)

@@ -57,6 +57,14 @@ def test_bench_line_contract():
     for k in ("one_shot", "one_shot_sdma_copy"):  # blit-kernel frame copy (the CLI's), runtime default (SDMA)
         os_ = d[k]
         assert os_["total_ms"] >= os_["render_ms"] > 0 and os_["context_ms"] > 0, (k, os_)
+    # the strong-scaling series at every N (here N = 1): configs[3] and [4] split by the group context
+    assert "NOT a scaling result" in d["scaling_note"]
+    assert set(d["tile_split"]) == {"cover", "table"}
+    for name, ts in d["tile_split"].items():
+        assert ts["config"]["width"] == 3840 and ts["config"]["height"] == 2160 and ts["config"]["scene"] == name
+        assert ts["scaling"] == "strong" and set(ts["gather_variants"]) == {"rccl", "peer"}
+        for k in ("render_ms_per_shard", "single_gpu_ms_per_step", "speedup_vs_1gpu", "value"):
+            assert ts[k] > 0, (name, k)
 
 
 @pytest.mark.gpu

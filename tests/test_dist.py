@@ -163,3 +163,50 @@ def test_camera_reaches_every_rank_bit_exact(tmp_path, rtc):
     ref = bytes(rtc.camera_resize(scene_fixture("cover").camera, 3840, 2160))
     for r in range(2):
         assert open(f"{out}.{r}", "rb").read() == ref
+
+
+def _fail_worker(rank, world, port, out_path):
+    """Rank 1's upload fails (a malformed table: RT_ERR_INVALID from the
+    library's validation, stood in for here since a group context needs GPUs);
+    the step's status agreement must make every rank raise, then a later
+    collective must still complete (nobody is left inside the failed step)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    import rtc_amd
+    from rtc_amd import dist as rdist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def upload():
+            if rank == 1:
+                raise rtc_amd.RenderError(rtc_amd.RT_ERR_INVALID, "shape 3: material index out of range")
+            return "uploaded"
+        try:
+            rdist.collective_call(upload, rank)
+            code = 0
+        except rtc_amd.RenderError as e:
+            code = e.code
+        t = torch.tensor([1.0])
+        dist.all_reduce(t)  # the group is still usable
+        with open(f"{out_path}.{rank}", "w") as f:
+            f.write(f"{code} {t.item()}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_a_rank_failing_its_upload_fails_every_rank(tmp_path):
+    import time
+
+    import torch.multiprocessing as mp
+    world = 2
+    out = str(tmp_path / "status")
+    t0 = time.monotonic()
+    ctx = mp.spawn(_fail_worker, args=(world, _free_port(), out), nprocs=world, join=False)
+    while not ctx.join(timeout=5):
+        assert time.monotonic() - t0 < 120, "a rank is still waiting after another failed its upload"
+    codes = [open(f"{out}.{r}").read().split() for r in range(world)]
+    assert int(codes[1][0]) == -1            # RT_ERR_INVALID on the failing rank
+    assert int(codes[0][0]) == -8            # RT_ERR_COMM on the others
+    assert all(float(c[1]) == 2.0 for c in codes)

@@ -193,13 +193,13 @@ def _render_with_env(rtc, monkeypatch, env, scene, cam, precision):
 @pytest.mark.parametrize("name", ["three_sphere_scene", "shadow_puppets", "cover", "table", "cylinders", "metal"])
 def test_cull_is_exact(gpu_ctx, rtc, monkeypatch, name, precision):
     """The wave cull is acceleration only: the frame with the cull off
-    (RTC_CULL=0: every shape uploaded as unbounded) equals the default frame
+    (RTC_DEBUG=cull=0: every shape uploaded as unbounded) equals the default frame
     bit for bit, counters included."""
     scene = scene_fixture(name)
     cam = rtc.camera_resize(scene.camera, 320, 200)
     gpu_ctx.upload(scene)
     a, sa = gpu_ctx.render(cam, 6, precision=precision)
-    b, sb = _render_with_env(rtc, monkeypatch, {"RTC_CULL": "0"}, scene, cam, precision)
+    b, sb = _render_with_env(rtc, monkeypatch, {"RTC_DEBUG": "cull=0"}, scene, cam, precision)
     assert np.array_equal(a, b), f"{name} {precision}: the cull changed {int((a != b).any(axis=2).sum())} px"
     assert _counts(sa) == _counts(sb)
 
@@ -208,12 +208,12 @@ def test_cull_is_exact(gpu_ctx, rtc, monkeypatch, name, precision):
 def test_kind_variant_is_exact(gpu_ctx, rtc, monkeypatch, name):
     """Worlds of spheres and planes run the pool kernel built with only those
     kinds' loops (rtc_kernels_sp.o): the same frame, bit for bit, as the
-    all-kinds kernel (RTC_KIND_VARIANTS=0), counters included."""
+    all-kinds kernel (RTC_DEBUG=kind_variants=0), counters included."""
     scene = scene_fixture(name)
     cam = rtc.camera_resize(scene.camera, 256, 160)
     gpu_ctx.upload(scene)
     a, sa = gpu_ctx.render(cam, 6, precision="f32")
-    b, sb = _render_with_env(rtc, monkeypatch, {"RTC_KIND_VARIANTS": "0"}, scene, cam, "f32")
+    b, sb = _render_with_env(rtc, monkeypatch, {"RTC_DEBUG": "kind_variants=0"}, scene, cam, "f32")
     assert np.array_equal(a, b) and _counts(sa) == _counts(sb)
 
 
@@ -221,7 +221,7 @@ def test_kind_variant_is_exact(gpu_ctx, rtc, monkeypatch, name):
 def test_cost_ordered_schedule_is_exact(gpu_ctx, rtc, monkeypatch, name):
     """Repeated launches of one frame run heaviest-tile-first from the last
     launch's per-tile costs (order_tiles): scheduling only — every ordered
-    render equals the raster-ordered render of a context with RTC_TILE_ORDER=0."""
+    render equals the raster-ordered render of a context with RTC_DEBUG=tile_order=0."""
     scene = scene_fixture(name)
     cam = rtc.camera_resize(scene.camera, 256, 160)
     gpu_ctx.upload(scene)
@@ -229,15 +229,15 @@ def test_cost_ordered_schedule_is_exact(gpu_ctx, rtc, monkeypatch, name):
     for _ in range(2):                                   # cost-ordered
         img, st = gpu_ctx.render(cam, 6, precision="f32")
         assert np.array_equal(img, first) and _counts(st) == _counts(s1)
-    raster, s0 = _render_with_env(rtc, monkeypatch, {"RTC_TILE_ORDER": "0"}, scene, cam, "f32")
+    raster, s0 = _render_with_env(rtc, monkeypatch, {"RTC_DEBUG": "tile_order=0"}, scene, cam, "f32")
     assert np.array_equal(raster, first) and _counts(s0) == _counts(s1)
 
 
 @pytest.mark.parametrize("shard", [(0, 1), (1, 4)])
 @pytest.mark.parametrize("name", ["reflect_refract", "cover"])
 def test_split_tiles_are_exact(rtc, monkeypatch, name, shard):
-    """Heavy tiles handed out in 2, 4, 8 or 16 parts (order_tiles; RTC_SPLIT tiny
-    splits nearly every tile 4 (RTC_SPLIT_MAX=3: 8, 4: 16) ways, at 1 every tile above the mean load),
+    """Heavy tiles handed out in 2, 4, 8 or 16 parts (order_tiles; split tiny
+    splits nearly every tile 4 (split_max=3: 8, 4: 16) ways, at 1 every tile above the mean load),
     then the frozen order reused (launches 4 and 5): every render equals the
     raster-ordered one bit for bit, counters included.  The first launch runs
     the centre-out cold order, later ones the costliest items at raised wave
@@ -245,12 +245,11 @@ def test_split_tiles_are_exact(rtc, monkeypatch, name, shard):
     scene = scene_fixture(name)
     cam = rtc.camera_resize(scene.camera, 256, 160)
     rows = rtc.shard_rows(cam.height, shard[1])
-    raster, s0 = _render_with_env(rtc, monkeypatch, {"RTC_TILE_ORDER": "0"}, scene, cam, "f32")
+    raster, s0 = _render_with_env(rtc, monkeypatch, {"RTC_DEBUG": "tile_order=0"}, scene, cam, "f32")
     raster = raster[:rows] if shard[1] == 1 else None
     for split, most in (("0.0001", "2"), ("1", "2"), ("0.0001", "3"), ("0.0001", "4"), ("1", "4")):
-        monkeypatch.setenv("RTC_TILE_ORDER", "1")
-        monkeypatch.setenv("RTC_SPLIT", split)
-        monkeypatch.setenv("RTC_SPLIT_MAX", most)  # up to 4, 8 (half-wave seeds) or 16 parts (wave-row seeds)
+        # up to 4, 8 (half-wave seeds) or 16 parts (wave-row seeds)
+        monkeypatch.setenv("RTC_DEBUG", f"tile_order=1,split={split},split_max={most}")
         with rtc.Context(0) as c:
             c.upload(scene)
             first, s1 = c.render(cam, 6, precision="f32", shard=shard)
@@ -286,7 +285,7 @@ def test_cull_is_exact_for_grazing_rays(gpu_ctx, rtc, monkeypatch, precision):
     rays = np.concatenate([o, d], axis=1)
     gpu_ctx.upload(tables)
     a, sa = gpu_ctx.color_at(rays, precision=precision)
-    monkeypatch.setenv("RTC_CULL", "0")
+    monkeypatch.setenv("RTC_DEBUG", "cull=0")
     with rtc.Context(0) as c:
         c.upload(tables)
         b, sb = c.color_at(rays, precision=precision)
@@ -429,7 +428,7 @@ def test_moved_camera_reuses_order_exactly(gpu_ctx, rtc, monkeypatch, name):
         for _ in range(3):  # the last two launches of each camera run an order built for it
             img, st = gpu_ctx.render(c, 6, precision="f32")
         ordered.append((img, st))
-    monkeypatch.setenv("RTC_TILE_ORDER", "0")
+    monkeypatch.setenv("RTC_DEBUG", "tile_order=0")
     with rtc.Context(0) as raster_ctx:
         raster_ctx.upload(scene)
         for c, (img, st) in zip(cams, ordered):

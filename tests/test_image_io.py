@@ -118,3 +118,14 @@ def test_errors(rtc, tmp_path):
         rtc.write_image(tmp_path / "file" / "x.png", np.zeros((2, 2, 3), dtype=np.uint8))
     with pytest.raises(rtc.RenderError):  # PNG of an empty canvas
         rtc.write_image(tmp_path / "e.png", np.zeros((0, 0, 3), dtype=np.uint8))
+
+
+def test_u8_frame_widened_to_a_canvas_saves_the_same_bytes(rtc, oracle):
+    """INTEGRATION.md 1b'': a Canvas built from the 8-bit frame as b / 255
+    quantizes back to b (canvas.rs:117-123) for every byte, so its PNG equals
+    the PNG of the f64 canvas the frame came from."""
+    b = np.arange(256, dtype=np.float64)
+    assert np.array_equal(oracle.quantize((b / 255.0).reshape(1, 256, 1)).ravel(), b.astype(np.uint8))
+    # and through the library's own quantizer (rt_canvas_quantize)
+    img = np.repeat((b / 255.0).reshape(1, 256, 1), 3, axis=2)
+    assert np.array_equal(rtc.canvas_quantize(img)[0, :, 0], b.astype(np.uint8))

@@ -57,8 +57,8 @@ def test_f32_kernels_stay_within_their_occupancy_budget(tmp_path):
 
 
 def test_static_lds_fits_the_hosts_allowance(tmp_path):
-    """rtc_host.cpp sizes LDS residency with kStaticLds = 256 B of static LDS
+    """rtc_host.cpp sizes LDS residency with kStaticLds = 512 B of static LDS
     per tracer workgroup; a kernel that declares more would be over-admitted."""
     for name, (_, _, group) in kernel_metadata(str(tmp_path)).items():
         if "trace_" in name:
-            assert group <= 256, f"{name}: {group} B of static LDS > kStaticLds"
+            assert group <= 512, f"{name}: {group} B of static LDS > kStaticLds"
