@@ -256,7 +256,10 @@ int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes,
     RT_HIP(hipMalloc(&w.image, std::max<size_t>(image_bytes, 16)));  // (an empty world still gets a buffer)
     if (image_bytes) RT_HIP(hipMemcpyAsync(w.image, img.data(), image_bytes, hipMemcpyHostToDevice, ctx->stream));
     w.carve(sh.size(), nm, np);
-    if ((rc = upload(&w.lights, lt, ctx->stream))) return rc;
+    if ((rc = upload(&w.lights, lt, ctx->stream))) {
+        (void)hipStreamSynchronize(ctx->stream);  // the image copy may still read `img`
+        return rc;
+    }
     RT_HIP(hipStreamSynchronize(ctx->stream));  // (img and lt are host temporaries)
     if constexpr (sizeof(R) == 4) {  // the per-scene build's tables (capture_jit_table), from the host copies
         ctx->jit_shapes = sh;
@@ -1181,14 +1184,23 @@ unsigned long long timeout_ticks(double timeout_ms) {  // s_memrealtime runs at 
     return timeout_ms < 0 ? ~0ull : (unsigned long long)(timeout_ms * 1e5);
 }
 
+// After a canvas's flags (n_flags ready flags + the release flag): a trailer
+// {image bytes, n_flags}, so rt_canvas_open can check the caller's sizes
+// against the creator's instead of placing its flags at a wrong offset.
+size_t canvas_flag_bytes(uint32_t n_flags) { return ((size_t)n_flags + 1 + 2) * sizeof(unsigned long long); }
+
 int canvas_create(rt_context* ctx, uint64_t bytes, uint32_t n_flags, void** canvas) {
     RT_HIP(hipSetDevice(ctx->device));
-    const size_t flag_bytes = ((size_t)n_flags + 1) * sizeof(unsigned long long);  // ready flags + release
+    const size_t flag_bytes = canvas_flag_bytes(n_flags);
     void* p = nullptr;
     RT_HIP(hipMalloc(&p, canvas_flag_offset(bytes) + flag_bytes));
-    if (hipError_t e = hipMemset(canvas_flags(p, bytes), 0, flag_bytes); e != hipSuccess) {
+    std::vector<unsigned long long> tail((size_t)n_flags + 3, 0ull);
+    tail[n_flags + 1] = bytes;
+    tail[n_flags + 2] = n_flags;
+    if (hipError_t e = hipMemcpy(canvas_flags(p, bytes), tail.data(), flag_bytes, hipMemcpyHostToDevice);
+        e != hipSuccess) {
         (void)hipFree(p);
-        return set_error(RT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e));
+        return set_error(RT_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
     }
     ctx->canvases[p] = {bytes, n_flags, true};
     *canvas = p;
@@ -1236,6 +1248,19 @@ int rt_canvas_open(rt_context* ctx, const uint8_t handle[RT_IPC_HANDLE_BYTES], u
     std::memcpy(&h, handle, sizeof h);
     void* p = nullptr;
     RT_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+    // the creator's sizes, from the canvas's trailer (inside the mapped range only)
+    hipDeviceptr_t base = nullptr;
+    size_t range = 0;
+    const size_t need = canvas_flag_offset(bytes) + canvas_flag_bytes(n_flags);
+    unsigned long long tail[2] = {0, 0};
+    const bool fits = hipMemGetAddressRange(&base, &range, (hipDeviceptr_t)p) == hipSuccess &&
+                      static_cast<char*>(p) + need <= static_cast<char*>(base) + range;
+    if (!fits || hipMemcpy(tail, canvas_flags(p, bytes) + n_flags + 1, sizeof tail, hipMemcpyDeviceToHost) != hipSuccess ||
+        tail[0] != bytes || tail[1] != n_flags) {
+        (void)hipIpcCloseMemHandle(p);
+        return set_error(RT_ERR_INVALID, "rt_canvas_open: bytes / n_flags differ from the creator's (" +
+                                             std::to_string(tail[0]) + " / " + std::to_string(tail[1]) + ")");
+    }
     ctx->canvases[p] = {bytes, n_flags, false};
     *canvas = p;
     return RT_OK;

@@ -655,6 +655,9 @@ struct Hit {
 template <typename R>
 struct Nearest {
     static constexpr bool kKeys = sizeof(R) == 4 && RTC_VALU_KEYS;
+    // per-scene records pack (world << 8 | slot) into the key's low word; only
+    // the key form decodes it (hit() below)
+    static_assert(!(kJitRecords && sizeof(R) == 4) || kKeys, "per-scene records need RTC_VALU_KEYS");
     R t = Real<R>::kInf;
     int w = __INT_MAX__;
     unsigned long long key = 0x7F8000007FFFFFFFull;  // (+inf, INT_MAX)
@@ -1395,8 +1398,15 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
         constexpr bool kTransparent = true;
 #endif
         const bool reflective = m.reflectiveness > (R)0, transparent = kTransparent && m.transparency > (R)0;
+        // n1 / n2 (the containers walk) feed only the children's weights and
+        // the refracted direction, and a ray at remaining 0 has no children
+        // (world.rs:120, 136): the walk runs for rays that can spawn.  (The
+        // reference computes them in every prepare_computations; the values are
+        // unused there too.)  The deepest generation is the largest one of a
+        // glass tree, so this skips most walks: DESIGN.md §3.2.
         R n1 = (R)1, n2 = (R)1;
-        if (kTransparent && m.transparency != (R)0) refractive_indices<R, kDup>(sc, o, d, h, q.mat, n1, n2);
+        if (kTransparent && m.transparency != (R)0 && remaining > 0)
+            refractive_indices<R, kDup>(sc, o, d, h, q.mat, n1, n2);
         // Schlick mixing only when both (world.rs:59-66)
         R fr = (R)1, ft = (R)1;
         if (reflective && transparent) {  // computed_hit.rs:50-68
@@ -2008,6 +2018,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
             };
             if (active) hit = shade_ray<R, true, kDup>(sc, ro, rd, meta >> 8, sh, push);
             count_events(k, false, hit, sh, sc.n_lights);
+#ifdef RTC_ITER_DIAG  // (diagnostic builds: lane slots and active lanes in place of counters 5 and 6)
+            k.c[5] += 64 - wave_count(hit & sh.patterned) * (uint32_t)sc.n_lights;
+            k.c[6] += wave_count(active) - wave_count(hit & sh.refr_eval);
+#endif
+#ifdef RTC_WALK_DIAG  // (diagnostic builds: waves that ran the walk x 64 and walking lanes in counters 5 and 6)
+            k.c[5] += (wave_any(hit & sh.schlick) ? 64u : 0u) - wave_count(hit & sh.patterned) * (uint32_t)sc.n_lights;
+            k.c[6] += wave_count(hit & sh.schlick) - wave_count(hit & sh.refr_eval);
+#endif
 #ifndef RTC_JIT  // (per-scene builds never take RT_FLAG_GENERATIONS launches)
             if (P.gen_counts) count_generations(P.gen_counts, active, hit, meta >> 8);
 #endif

@@ -114,3 +114,40 @@ def test_render_to_canvas_validates(gpu_ctx, rtc):
         assert np.array_equal(gpu_ctx.canvas_read(canvas, ref.shape), ref)
     finally:
         gpu_ctx.canvas_close(canvas)
+
+
+OPEN_CHILD = r"""
+import json, os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "ray-tracer-challenge-rs_amd"))
+import rtc_amd
+req = json.loads(sys.stdin.readline())
+ctx = rtc_amd.Context(0)
+res = []
+for nbytes, n_flags in req["tries"]:
+    try:
+        c = ctx.canvas_open(bytes.fromhex(req["handle"]), nbytes, n_flags)
+        ctx.canvas_close(c)
+        res.append("ok")
+    except rtc_amd.RenderError as e:
+        res.append(e.code)
+ctx.close()
+print(json.dumps(res), flush=True)
+"""
+
+
+def test_canvas_open_checks_the_creators_sizes(gpu_ctx, rtc):
+    """rt_canvas_open reads the canvas's trailer (image bytes, flag count) and
+    refuses sizes that differ from the creator's (a wrong
+    `bytes` would have put the opener's flags at a wrong offset)."""
+    nbytes, shards = 3840 * 2160 * 3, 8
+    canvas, handle = gpu_ctx.canvas_create(nbytes, shards)
+    try:
+        tries = [(nbytes, shards), (nbytes - 256, shards), (nbytes + 4096, shards), (nbytes, shards - 1),
+                 (nbytes * 2, shards)]
+        r = subprocess.run([sys.executable, "-c", OPEN_CHILD, ROOT], input=json.dumps(
+            {"handle": handle.hex(), "tries": tries}) + "\n", capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-3000:]
+        got = json.loads(r.stdout.strip().splitlines()[-1])
+        assert got[0] == "ok" and got[1:] == [rtc.RT_ERR_INVALID] * 4, got
+    finally:
+        gpu_ctx.canvas_close(canvas)
