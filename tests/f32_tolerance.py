@@ -1,0 +1,53 @@
+"""The f32 path's tolerance against the f64 oracle, per scene: the observed
+values (profiles/r05_parity.json: scripts/parity_report.py at 160x120,
+320x200 and the BASELINE configs' own sizes, round 5) plus a stated margin.
+
+  pix2   fraction of pixels within 2/255 after the reference's quantization
+         (canvas.rs:117-123): the smallest observed, minus 0.001 (0.002 at
+         160x120 and below, where one pixel is 1/19200 of the frame)
+  mean   mean |err| over the frame: twice the largest observed
+  kind   |gpu - oracle| / oracle per ray kind (primary, shadow, reflect,
+         refract): 2e-3 (largest observed 1.2e-3, cylinders' reflect at
+         160x120), except where the scene's f32 decisions diverge more:
+         table's glass cube refracts 2.7-3.0 % fewer rays in f32 (TIR and
+         containers decisions at its faces after the f32 surface offset;
+         DESIGN.md §4), held to 3.5 %
+  rays   total rays per frame: 1e-3 (largest observed 3e-4)
+
+The residual mismatches sit on silhouettes, shadow terminators and pattern
+edges where an f32 rounding flips a branch, and where f32 needs its own
+over/under-point offset (3e-5 x max(1, |p|inf) instead of 8e-8, below the f32
+ulp at |p| > 0.7; DESIGN.md §4 has the study that chose it).
+"""
+# scene -> (pix2 floor, mean bound); observed (min pix2, max mean) in the comments
+PIX_MEAN = {
+    "three_sphere_scene": (0.999, 5e-5),   # 0.99995, 2.4e-5
+    "reflect_refract": (0.998, 4e-5),      # 0.99974, 1.7e-5
+    "cover": (0.998, 3e-5),                # 0.99984, 1.1e-5
+    "table": (0.997, 8e-5),                # 0.99890, 3.8e-5
+    "cylinders": (0.994, 1.5e-3),          # 0.99642, 7.1e-4
+    "metal": (0.998, 2e-5),                # 0.99998, 6.1e-6
+    "refraction": (0.972, 3e-3),           # 0.97605, 1.5e-3 (the lens magnifies the offset)
+    "shadow_puppets": (0.999, 1e-5),       # 1.0, 3.4e-7
+}
+KIND = 2e-3
+KIND_SCENE = {("table", "refract"): 0.035}
+RAYS = 1e-3
+
+
+def pix_floor(name, pixels):
+    frac, _ = PIX_MEAN.get(name, (0.99, 2e-3))
+    return frac - (0.001 if pixels <= 160 * 120 else 0.0)
+
+
+def check(name, agree2, mean, st, rst, pixels):
+    """Assert the f32 frame's statistics against the oracle's (rt_stats dicts)."""
+    frac = pix_floor(name, pixels)
+    _, mean_bound = PIX_MEAN.get(name, (0.99, 2e-3))
+    assert agree2 >= frac, f"{name}: {agree2:.5f} of pixels within 2/255 (floor {frac})"
+    assert mean < mean_bound, f"{name}: mean |err| {mean:.3g} (bound {mean_bound})"
+    assert abs(st["rays"] - rst["rays"]) <= RAYS * rst["rays"], (name, st["rays"], rst["rays"])
+    for k in ("primary", "shadow", "reflect", "refract"):
+        tol = KIND_SCENE.get((name, k), KIND)
+        # (a floor of 3 rays: a kind with a few hundred rays flips single spawns)
+        assert abs(st[k] - rst[k]) <= max(3, tol * rst[k]), (name, k, st[k], rst[k], tol)
