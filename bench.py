@@ -36,6 +36,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -140,7 +141,6 @@ def cpu_serial_configs0(budget_s):
         _, st = pyoracle.render(scene, cam, 6, threads=1)
         times.append(time.perf_counter() - t)
         rays += st["rays"]
-    import statistics
     ms = statistics.median(times) * 1e3
     return {"config": "scenes/three_sphere_scene.yaml at 320x240, serial CPU mode (BASELINE configs[0])",
             "ms_per_frame": ms, "value": rays / sum(times) / 1e6, "unit": "Mray/s", "cores": 1,
@@ -231,20 +231,33 @@ def one_shot_child(args):
     ctx.close()
 
 
-def one_shot(args, env=None):
-    """Run one_shot_child in a subprocess (rank 0, N = 1); None if it fails.
-    `env`: extra environment of the child (the SDMA-copy variant)."""
+def one_shot(args, env=None, runs=3):
+    """Run one_shot_child in `runs` fresh subprocesses (rank 0, N = 1) and
+    report the median of each timing (a single start-up sample varies by
+    2x between runs); {"error": ...} if a run fails.  `env`: extra
+    environment of the child (the SDMA-copy variant)."""
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--one-shot-child", "--precision", args.precision]
     for k in ("scene", "width", "height", "depth"):
         if getattr(args, k) is not None:
             cmd += [f"--{k}", str(getattr(args, k))]
+    samples = []
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env={**os.environ, **(env or {})})
-        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-        return json.loads(lines[-1]) if r.returncode == 0 and lines else {"error": (r.stderr or r.stdout)[-400:]}
+        for _ in range(runs):
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env={**os.environ, **(env or {})})
+            lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            if r.returncode != 0 or not lines:
+                return {"error": (r.stderr or r.stdout)[-400:]}
+            samples.append(json.loads(lines[-1]))
     except Exception as e:  # noqa: BLE001  (a diagnostic: never fails the bench line)
         return {"error": repr(e)[:400]}
+    out = dict(samples[0])
+    for k, v in samples[0].items():
+        if isinstance(v, float):
+            out[k] = float(statistics.median(s[k] for s in samples))
+    out["runs"] = runs
+    out["total_ms_samples"] = [round(s["total_ms"], 2) for s in samples]
+    return out
 
 
 def main():

@@ -24,7 +24,9 @@
 static int usage() {
     std::fprintf(stderr,
                  "usage: rtc <SCENE.yaml> <OUT.png|OUT.ppm> [-r serial|parallel|gpu] [-q] [--width W] [--height H]\n"
-                 "           [--depth D] [--precision f32|f64] [--device N] [--gpus N] [--ppm-binary] [--timings]\n");
+                 "           [--depth D] [--precision f32|f64] [--device N] [--gpus N] [--ppm-binary] [--timings]\n"
+                 "  -r serial|parallel are accepted for the reference's command lines but render on the GPU like\n"
+                 "  -r gpu: this build ships no CPU renderer (Camera::render / render_parallel are not in it).\n");
     return 2;
 }
 

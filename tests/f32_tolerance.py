@@ -8,10 +8,13 @@ values (profiles/r05_parity.json: scripts/parity_report.py at 160x120,
   mean   mean |err| over the frame: twice the largest observed
   kind   |gpu - oracle| / oracle per ray kind (primary, shadow, reflect,
          refract): 2e-3 (largest observed 1.2e-3, cylinders' reflect at
-         160x120), except where the scene's f32 decisions diverge more:
-         table's glass cube refracts 2.7-3.0 % fewer rays in f32 (TIR and
-         containers decisions at its faces after the f32 surface offset;
-         DESIGN.md §4), held to 3.5 %
+         160x120), except table's refractions, 2.7-3.0 % fewer in f32 and
+         held to 3.5 %: table.yaml:131-136 floats the glass cube 1e-5 above
+         the table top, a tenth of the f32 surface offset there (3e-5 x 3.45),
+         so rays reflected off the table under the cube start inside the
+         glass instead of entering it through its bottom face (the f64
+         oracle built with the same offset loses the same 62 of 2040 at
+         320x200: tests/study_offset_oracle.py)
   rays   total rays per frame: 1e-3 (largest observed 3e-4)
 
 The residual mismatches sit on silhouettes, shadow terminators and pattern

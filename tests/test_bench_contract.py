@@ -57,6 +57,7 @@ def test_bench_line_contract():
     for k in ("one_shot", "one_shot_sdma_copy"):  # blit-kernel frame copy (the CLI's), runtime default (SDMA)
         os_ = d[k]
         assert os_["total_ms"] >= os_["render_ms"] > 0 and os_["context_ms"] > 0, (k, os_)
+        assert os_["runs"] == 3 and len(os_["total_ms_samples"]) == 3  # median of three fresh processes
     # the strong-scaling series at every N (here N = 1): configs[3] and [4] split by the group context
     assert "NOT a scaling result" in d["scaling_note"]
     assert set(d["tile_split"]) == {"cover", "table"}

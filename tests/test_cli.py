@@ -60,7 +60,9 @@ def read_ppm(path, magic=b"P3"):
 
 
 def test_cli_usage_and_missing_scene_fail_loudly(tmp_path):
-    assert subprocess.run([CLI], capture_output=True).returncode != 0
+    r = subprocess.run([CLI], capture_output=True, text=True)
+    # -r serial|parallel render on the GPU too, and the help says so (no CPU renderer ships)
+    assert r.returncode != 0 and "no CPU renderer" in r.stderr
     assert subprocess.run([CLI, "a.yaml", "b.png", "-r", "bogus"], capture_output=True).returncode == 2
     r = subprocess.run([CLI, str(tmp_path / "missing.yaml"), str(tmp_path / "o.ppm")], capture_output=True, text=True)
     assert r.returncode != 0 and "error" in r.stderr
