@@ -1189,11 +1189,18 @@ unsigned long long timeout_ticks(double timeout_ms) {  // s_memrealtime runs at 
 // against the creator's instead of placing its flags at a wrong offset.
 size_t canvas_flag_bytes(uint32_t n_flags) { return ((size_t)n_flags + 1 + 2) * sizeof(unsigned long long); }
 
+// The canvas is fine-grained device memory: other GPUs store pixels and
+// flags into it over xGMI while the owner's canvas_wait polls the flags, and
+// the owner then copies the image out.  In coarse-grained memory the owner's
+// L2 may keep a line (a flag it polled, pixels it copied out last frame) that
+// a peer's store to HBM never updates, and a system-scope acquire does not
+// invalidate such lines; fine-grained lines are the ones its acquire
+// (canvas_wait) invalidates and its kernels' releases write back.
 int canvas_create(rt_context* ctx, uint64_t bytes, uint32_t n_flags, void** canvas) {
     RT_HIP(hipSetDevice(ctx->device));
     const size_t flag_bytes = canvas_flag_bytes(n_flags);
     void* p = nullptr;
-    RT_HIP(hipMalloc(&p, canvas_flag_offset(bytes) + flag_bytes));
+    RT_HIP(hipExtMallocWithFlags(&p, canvas_flag_offset(bytes) + flag_bytes, hipDeviceMallocFinegrained));
     std::vector<unsigned long long> tail((size_t)n_flags + 3, 0ull);
     tail[n_flags + 1] = bytes;
     tail[n_flags + 2] = n_flags;

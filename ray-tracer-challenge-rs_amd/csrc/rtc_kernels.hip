@@ -596,11 +596,21 @@ __device__ inline void jit_members(F&& f) {
         jit_members<C, M + 1>(f);
     }
 }
+// a cluster of spheres and cubes only (the walk's point test, refractive_indices)
+template <int C>
+constexpr bool jit_cluster_convex() {
+    for (int m = jit::kClusterBegin[C]; m < jit::kClusterBegin[C + 1]; ++m) {
+        const int k = jit_kind_of(jit::kClusterMembers[m]);
+        if (k != RT_SHAPE_SPHERE && k != RT_SHAPE_CUBE) return false;
+    }
+    return true;
+}
 template <bool kHalfLine, int C, typename F, typename S>
 __device__ inline void jit_clusters(V3<float>& o, V3<float>& d, float dd, F&& f, S&& skip) {
     if constexpr (C < jit::kNumClusters) {
         jit_fence(o, d);
-        if (!skip(jit::kClusterBall[C][0], jit::kClusterBall[C][1], jit::kClusterBall[C][2], jit::kClusterBall[C][3]) &&
+        if (!skip(jit::kClusterBall[C][0], jit::kClusterBall[C][1], jit::kClusterBall[C][2], jit::kClusterBall[C][3],
+                  jit_cluster_convex<C>()) &&
             wave_ball_may_hit<float, kHalfLine>(jit::kClusterBall[C][0], jit::kClusterBall[C][1], jit::kClusterBall[C][2],
                                                 jit::kClusterBall[C][3], o, d, dd))
             jit_members<C, jit::kClusterBegin[C]>(f);
@@ -608,8 +618,9 @@ __device__ inline void jit_clusters(V3<float>& o, V3<float>& d, float dd, F&& f,
     }
 }
 #endif
-// `skip(centre, r^2)`: a caller's wave-uniform reason to pass a cluster by
-// before its ball test (none by default).
+// `skip(centre, r^2, convex)`: a caller's wave-uniform reason to pass a
+// cluster by before its ball test (none by default); `convex`: every member
+// is a sphere or a cube.
 struct NoSkip {
     template <typename... A>
     __device__ bool operator()(A...) const {
@@ -812,7 +823,7 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist, 
     // the answer (per cluster, not per shape: a per-shape check measured
     // slower in round 3; per cluster cover -2.5 %, cylinders -4 %, table +1 %)
     const bool skips = skips_on(sc);
-    auto skip = [&](R, R, R, R) { return skips && !wave_any(!b.blocked(dist)); };
+    auto skip = [&](R, R, R, R, bool) { return skips && !wave_any(!b.blocked(dist)); };
     for_all_culled<R, true>(sc, o, d, dd, [&]<int K>(const ShapeRec<R>& s, int slot) {
         if (!s.casts_shadow) return;  // wave-uniform
         jit_fence(o, d, slot);
@@ -954,12 +965,45 @@ __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> 
             count = 0;
         });
     } else if constexpr (kWalkCull) {  // (line culls: clusters too in per-scene builds)
+        // Only a shape with an odd count of entries before the hit is settled.
+        // A sphere's or cube's two entries t1 <= t2 share one validity, so its
+        // count is odd only when t1 sorts before the hit and t2 does not: the
+        // hit point p = o + t d lies between them, inside the shape.  A sphere
+        // or cube (or a cluster of them) whose padded ball holds no active
+        // lane's p, and which is no lane's hit shape, settles nothing and is
+        // skipped: a test of p against the ball in place of the line test,
+        // and far stronger (the line passes near many shapes its hit point is
+        // nowhere near).  Conservative like the line test: the pad
+        // (rtc_host.cpp bounding_sphere, >= 1e-4 of the ball's distance from
+        // the origin) dwarfs p's rounding, and |p - c|^2 is shrunk by kKeep.
+        // Other kinds keep the line test: an open cylinder's or cone's walls,
+        // and a triangle, leave odd counts far from the shape (one entry
+        // before the hit, the other missing).  Frames equal the line-culled
+        // walk's bit for bit (tests/test_gpu_skips.py renders against
+        // RT_FLAG_NO_SKIPS, which keeps the line test).
+        const bool points = skips_on(sc);
+        // (p - c formed per test from o, d and t, which stay live for the
+        // scans anyway: a p held across the walk spilled in cover's build)
+        auto holds = [&](R cx, R cy, R cz, R r2) {
+            constexpr R kKeep = sizeof(R) == 4 ? (R)(1 - 1e-5) : (R)(1 - 1e-12);
+            const V3<R> pc = {Real<R>::madd(h.t, d.x, o.x - cx), Real<R>::madd(h.t, d.y, o.y - cy),
+                              Real<R>::madd(h.t, d.z, o.z - cz)};
+            return wave_any(dot(pc, pc) * kKeep <= r2);
+        };
         for_all_culled<R, false>(sc, o, d, dd, [&]<int K>(const ShapeRec<R>& s, int slot) {
-            if (!wave_line_may_hit<R, K>(s, o, d, dd)) return;  // no entries: nothing to settle
+            if (points && (K == RT_SHAPE_SPHERE || K == RT_SHAPE_CUBE)) {
+                if (!holds(s.bound[0], s.bound[1], s.bound[2], s.bound[3]) && !wave_any(slot == h.slot)) return;
+            } else if (!wave_line_may_hit<R, K>(s, o, d, dd)) {
+                return;  // no entries: nothing to settle
+            }
             int count = 0;
             Key last{};
             scan.template operator()<K>(s, count, last);
             settle(count, last, s, slot == h.slot);
+        }, [&](R cx, R cy, R cz, R r2, bool convex) {
+            // a cluster of spheres and cubes whose ball holds no lane's p (a
+            // hit shape's own ball holds its p, so the hit's cluster stays)
+            return points && convex && !holds(cx, cy, cz, r2);
         });
     } else {
         for_all_kinds<R>(sc, [&]<int K>(const ShapeRec<R>& s, int slot) {

@@ -9,7 +9,9 @@ fraction (which credits every cull as achieved work):
   valu_issue_frac = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x kernel cycles at 2.4 GHz)
   wait_frac       = SQ_WAIT_ANY / SQ_WAVE_CYCLES
 
-Usage: python scripts/collect_profiles.py r02
+Usage: python scripts/collect_profiles.py r02 [OUT_DIR]
+(OUT_DIR default profiles/; on a GPU box, a directory under gpurun_out/ that
+then comes back instead of the raw traces, which exceed gpurun's 64 MiB)
 """
 import collections
 import csv
@@ -55,12 +57,16 @@ def kernel_medians(d):
 
 def main():
     rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
-    out = os.path.join(ROOT, "profiles")
+    out = os.path.abspath(sys.argv[2]) if len(sys.argv) > 2 else os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
-    tp = os.path.join(out, "traffic.json")
-    traffic = json.load(open(tp)) if os.path.exists(tp) else {}
-    ip = os.path.join(out, "issue.json")
-    issue = json.load(open(ip)) if os.path.exists(ip) else {}
+
+    def prior(name):  # the tracked file's entries, updated by this round's
+        for p in (os.path.join(out, name), os.path.join(ROOT, "profiles", name)):
+            if os.path.exists(p):
+                return json.load(open(p))
+        return {}
+    tp, ip = os.path.join(out, "traffic.json"), os.path.join(out, "issue.json")
+    traffic, issue = prior("traffic.json"), prior("issue.json")
     for key, workload in SCENES.items():
         src = os.path.join(ROOT, "gpurun_out", f"{rnd}_stats_{key}")
         for f in glob.glob(os.path.join(src, "**", "*kernel_stats.csv"), recursive=True):
