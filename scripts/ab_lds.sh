@@ -7,7 +7,7 @@ source scripts/ab_lib.sh
 B="python bench.py --steps 60 --warmup 10 --no-cpu-baseline"
 for sc in three_sphere_scene reflect_refract cover table shadow_puppets cylinders metal refraction; do
   for l in 1 0; do
-    run "lds=$l $sc f32" env RTC_LDS_WORLD=$l $B --scene $sc
+    run "lds=$l $sc f32" env RTC_DEBUG=lds_world=$l $B --scene $sc
   done
 done
 run "lds=1 three_sphere f64" $B --precision f64

@@ -77,13 +77,13 @@ for step in "$@"; do
       mkdir -p gpurun_out/jit
       for a in "--scene three_sphere_scene" "--scene reflect_refract" "--scene cover --width 3840 --height 2160" \
                "--scene table --width 3840 --height 2160"; do
-        RTC_JIT_DUMP=gpurun_out/jit RTC_JIT_CACHE=0 timeout -k 10 200 python bench.py $a --steps 20 --no-cpu-baseline \
+        RTC_DEBUG=jit_dump=gpurun_out/jit RTC_JIT_CACHE=0 timeout -k 10 200 python bench.py $a --steps 20 --no-cpu-baseline \
           > /dev/null 2>>gpurun_out/jitdump.log || { echo "jitdump $a failed"; exit 1; }
       done
       ls gpurun_out/jit ;;
-    oneshot)  # where a one-shot render's time goes (RTC_TRACE_INIT steps), torch-free child, twice
+    oneshot)  # where a one-shot render's time goes (RTC_DEBUG=trace_init steps), torch-free child, twice
       for i in 1 2; do
-        RTC_TRACE_INIT=1 timeout -k 10 120 python bench.py --one-shot-child > gpurun_out/oneshot_$i.log 2>&1
+        RTC_DEBUG=trace_init=1 timeout -k 10 120 python bench.py --one-shot-child > gpurun_out/oneshot_$i.log 2>&1
         rc=$?; echo "oneshot rc=$rc"; grep -v amdgpu.ids gpurun_out/oneshot_$i.log; [ $rc -eq 0 ] || exit $rc
       done ;;
     initprobe)  # start-up steps of a bare HIP process (scripts/init_probe.cpp), with and without RCCL loaded
@@ -107,7 +107,7 @@ for step in "$@"; do
     shardtail)  # item log of shard 0 of 8 (cover 4K) at split 8 and 16
       : > gpurun_out/shardtail.log
       for sm in 3 4; do
-        RTC_SPLIT_MAX=$sm timeout -k 10 300 python scripts/shard_tail.py cover 3840 2160 8 0 >> gpurun_out/shardtail.log 2>&1
+        RTC_DEBUG=split_max=$sm timeout -k 10 300 python scripts/shard_tail.py cover 3840 2160 8 0 >> gpurun_out/shardtail.log 2>&1
         rc=$?; [ $rc -eq 0 ] || { echo "shardtail rc=$rc"; tail -5 gpurun_out/shardtail.log; exit $rc; }
       done
       grep -v amdgpu.ids gpurun_out/shardtail.log | cut -c1-1500 ;;

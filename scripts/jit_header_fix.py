@@ -1,6 +1,6 @@
 """Add the tables a newer kernel source expects (kMaterials; the shape clusters,
 computed as rtc_jit.cpp make_clusters does) to a per-scene header dumped by an
-older build (RTC_JIT_DUMP), from the scene's fixture, so scripts/jit_isa.sh can
+older build (RTC_DEBUG=jit_dump=<dir>), from the scene's fixture, so scripts/jit_isa.sh can
 compile it.  ISA inspection only.
 Usage: python scripts/jit_header_fix.py <dumped.hpp> <scene name> > fixed.hpp"""
 import json

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Device ISA of a per-scene (hipRTC) build, made here with hipcc from a scene
-# header dumped on the GPU box (RTC_JIT_DUMP=<dir>: <key>_direct.hpp /
+# header dumped on the GPU box (RTC_DEBUG=jit_dump=<dir>: <key>_direct.hpp /
 # <key>_pool.hpp).  Same source, defines and flags as rtc_jit.cpp
 # make_request; prints the instruction-class counts of scripts/isa_stats.sh.
 #   scripts/jit_isa.sh <scene.hpp> [out.s] [extra hipcc flags...]

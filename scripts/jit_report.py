@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostic: which frames run a per-scene kernel (rt_jit_status) and, with
-RTC_JIT_DUMP=<dir>, the generated scene headers and code objects.
+RTC_DEBUG=jit_dump=<dir>, the generated scene headers and code objects.
 
 Usage: [JIT_PRECISION=f64] jit_report.py [scene[:WxH] ...]
 """

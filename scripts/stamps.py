@@ -54,7 +54,7 @@ def main():
         ctx.render_device(cam, out.data_ptr(), 0, 6, args.precision, args.out, (si, sn), args.flags)
     ev[1].record()
     torch.cuda.synchronize()
-    res = {"label": f"{args.scene} flags={args.flags} out={args.out} sched={os.environ.get('RTC_SCHED_DIRECT', 'default')}",
+    res = {"label": f"{args.scene} flags={args.flags} out={args.out} sched={os.environ.get('RTC_DEBUG', 'default')}",
            "launch_us": round(ev[0].elapsed_time(ev[1]) * 1e3 / 50, 2),
            "workgroups": int(len(st)), "span_us": round(float(end.max()), 2),
            "start_q_us": q(start), "dur_q_us": q(dur), "end_q_us": q(end)}
