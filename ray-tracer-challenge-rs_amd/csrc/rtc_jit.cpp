@@ -57,6 +57,7 @@
 #include <unistd.h>
 
 #include "debug_knobs.hpp"
+#include "jit_options.hpp"
 #include "rtc_context.hpp"
 #include "rtc_jit_cache.hpp"
 #include "rtc_jit_sources.inc"  // kSrcKernels, kSrcInternal, kSrcRtcH, kBuildExtra (tools/embed_sources.py)
@@ -402,20 +403,9 @@ jitfile::Request make_request(const std::string& scene, const char* name, const 
                "-disable-machine-licm"};
     static const std::vector<std::string> defines = build_defines();
     rq.opts.insert(rq.opts.end(), defines.begin(), defines.end());
-    // The direct kernel fences the ray at every third shape only: the shape
-    // tests in between may interleave (more ILP) and still fit 8 waves/SIMD
-    // without spilling.  Same-box A/B against a fence per shape: shadow_puppets
-    // -3.6 %, three_sphere 4K -2.5 %, 1080p -0.6 %; the pool kernel lost 15 %
-    // on cover that way and keeps a fence per shape.
-    if (!std::strstr(name, "pool")) rq.opts.push_back("-DRTC_JIT_FENCE_EVERY=3");
-    // RT_FLAG_NO_SKIPS launches (exactness tests) run a build without the skips
-    if (no_skips) rq.opts.push_back("-DRTC_NO_SKIPS");
-    // Shape records as constants (rtc_kernels.hip kJitRecords) pay off in the
-    // direct kernel only.  Same-box A/B, two rounds (profiles/ab/r04_ab_builds.log):
-    // direct three_sphere 17.0 us with them vs 18.4 us without; pool kernels
-    // without them reflect_refract -3.0 %, table -1.2 %, cover -0.6 % (the
-    // per-slot branches cost more than the extra LDS pool slots gain).
-    else rq.opts.push_back("-DRTC_JIT_NO_RECORDS");
+    // per kind: fence spacing, records as constants, the no-skips build
+    const auto kind = jit_kind_defines(std::strstr(name, "pool") != nullptr, no_skips);
+    rq.opts.insert(rq.opts.end(), kind.begin(), kind.end());
     // RTC_DEBUG=jit_flags=...: extra compiler options, space-separated (A/B diagnostics)
     if (std::string all; debug_knob("jit_flags", &all)) {
         for (size_t p = 0; p < all.size();) {

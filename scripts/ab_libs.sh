@@ -5,7 +5,7 @@
 #   VARIANTS="_lib_base _lib" SCENES="rr cover table" bash scripts/ab_libs.sh   (on a GPU box)
 set -u
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-b() { local tag=$1; shift; timeout -k 10 60 python bench.py --ab --no-cpu-baseline "$@" 2>gpurun_out/ab.err | grep '^{' | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag', d['config']['workload'][:22], round(d['roofline']['kernel_ms'],4), 'cold', round(d.get('cold_kernel_ms') or 0,4))" || { tail -3 gpurun_out/ab.err; return 1; }; }
+b() { local tag=$1; shift; timeout -k 10 60 python bench.py --ab --mode frames --no-cpu-baseline "$@" 2>gpurun_out/ab.err | grep '^{' | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag', d['config']['workload'][:22], round(d['roofline']['kernel_ms'],4), 'cold', round(d.get('cold_kernel_ms') or 0,4))" || { tail -3 gpurun_out/ab.err; return 1; }; }
 for r in 1 2; do
 for v in ${VARIANTS:-_lib_base _lib}; do
   export RTC_LIBRARY=$GRAFT_REPO_ROOT/ray-tracer-challenge-rs_amd/rtc_amd/$v/librtc.so
