@@ -143,6 +143,37 @@ void bounding_sphere(const rt_shape_desc& d, double out[4]) {
     out[3] = wr + pad;
 }
 
+// A sphere whose transformation is a similarity (rotation, uniform scale,
+// translation): its world centre and radius^2, for the f32 kernels' roots in
+// world space (rtc_internal.hpp kShapeSimilar, rtc_kernels.hip sphere_world).
+// The linear part L of the forward transformation must satisfy
+// L^T L = s^2 I to 1e-9 of s^2, far below the f32 rounding the kernels work
+// at; shadow_puppets.yaml's backdrop (scaled 0.01 in z) keeps the
+// object-space test.
+bool similar_sphere(const rt_shape_desc& d, double centre[3], double* r2) {
+    if (d.kind != RT_SHAPE_SPHERE) return false;
+    hm::M4 inv;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) inv.m[i][j] = d.inverse[4 * i + j];
+    if (inv.m[3][0] != 0.0 || inv.m[3][1] != 0.0 || inv.m[3][2] != 0.0 || inv.m[3][3] != 1.0) return false;
+    const hm::M4 f = hm::inverse(inv);
+    double g[3][3] = {};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) g[i][j] += f.m[k][i] * f.m[k][j];
+    const double s2 = (g[0][0] + g[1][1] + g[2][2]) / 3.0;
+    if (!(s2 > 0.0) || !std::isfinite(s2)) return false;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            if (!(std::fabs(g[i][j] - (i == j ? s2 : 0.0)) <= 1e-9 * s2)) return false;
+    for (int i = 0; i < 3; ++i) {
+        centre[i] = f.m[i][3];
+        if (!std::isfinite(centre[i])) return false;
+    }
+    *r2 = s2;
+    return true;
+}
+
 // Device table order: by kind, then by identity class (the world index of
 // the class's first shape), then by world index.  Without value-equal shapes
 // this is world order within each kind.  The tie rule never depends on the
@@ -190,10 +221,16 @@ int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes,
                 r.tri[6 + q] = (R)d.edge_2[q];
                 r.tri[9 + q] = (R)d.normal[q];
             }
+            double centre[3], r2 = 0.0;
+            const bool similar = similar_sphere(d, centre, &r2);
+            if (similar) {
+                for (int q = 0; q < 3; ++q) r.tri[q] = (R)centre[q];
+                r.tri[3] = (R)r2;
+            }
             r.world_index = (int32_t)i;
             r.material = d.material;
             const bool class_end = next + 1 >= order.size() || cls[order[next + 1]] != cls[i];
-            r.flags = (d.closed ? kShapeClosed : 0) | (class_end ? kShapeClassEnd : 0) |
+            r.flags = (d.closed ? kShapeClosed : 0) | (class_end ? kShapeClassEnd : 0) | (similar ? kShapeSimilar : 0) |
                       (int32_t)(cls[i] << kShapeClassShift);
             r.casts_shadow = mats[d.material].casts_shadow ? 1 : 0;
             sh.push_back(r);

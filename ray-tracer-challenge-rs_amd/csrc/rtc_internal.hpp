@@ -213,6 +213,11 @@ static_assert(RT_MAX_SUPPORTED_DEPTH < 32, "remaining must fit the pool meta's 8
 // no value-equal shapes has one class per shape, each its own world index.
 constexpr int32_t kShapeClosed = 1;    // cylinder/cone `closed`
 constexpr int32_t kShapeClassEnd = 2;  // last member of its identity class
+// A sphere whose transformation is a similarity (rotation, uniform scale,
+// translation: rtc_host.cpp similar_sphere): tri[0..2] holds its world
+// centre and tri[3] its radius^2, and the f32 kernels find its roots in world
+// space (rtc_kernels.hip sphere_world).
+constexpr int32_t kShapeSimilar = 4;
 constexpr int kShapeClassShift = 8;
 
 template <typename R>
@@ -228,7 +233,8 @@ struct alignas(16) ShapeRec {
     int32_t material;
     int32_t flags;  // kShapeClosed | kShapeClassEnd | identity class << kShapeClassShift
     R ymin, ymax;  // cylinder/cone min/max (cylinder.rs:12-14)
-    R tri[12];     // triangle vertex_1, edge_1, edge_2, normal (triangle.rs:12-17)
+    R tri[12];     // triangle vertex_1, edge_1, edge_2, normal (triangle.rs:12-17);
+                   // a kShapeSimilar sphere: world centre, radius^2
 };
 
 template <typename R>

@@ -482,6 +482,42 @@ __device__ inline void for_all_kinds(const DevScene<R>& sc, F&& f) {
                                    [&](const ShapeRec<R>& s, int i) { f.template operator()<RT_SHAPE_TRIANGLE>(s, i); });
 }
 
+// The roots of a kShapeSimilar sphere (f32), in world space: with oc = c - o
+// and a = |d|^2, a t^2 - 2 t d.oc + |oc|^2 - r^2 = 0, whose discriminant is
+// a r^2 - |d x oc|^2 (Lagrange's identity, as entries() forms it in object
+// space), so t = (d.oc -+ sqrt(a r^2 - |d x oc|^2)) / a.  The same line and
+// sphere as the object-space test (the transformation maps one onto the
+// other), without transforming the ray: 3 subtractions instead of a point and
+// a vector through the matrix, and 1/a once per ray (rdd) instead of a
+// reciprocal per sphere.  f32 only: the f64 path keeps the reference's
+// object-space arithmetic (its decisions must equal the oracle's).
+template <typename R, bool kNearest, typename F>
+__device__ inline void sphere_world(const ShapeRec<R>& s, V3<R> o, V3<R> d, R dd, R rdd, F&& emit) {
+    const V3<R> oc = {s.tri[0] - o.x, s.tri[1] - o.y, s.tri[2] - o.z};
+    const R tc = dot(d, oc);
+    const V3<R> c = cross(d, oc);
+    const R disc = s.tri[3] * dd - dot(c, c);
+    const bool v = !(disc < (R)0);
+    const R root = Real<R>::sqrt(disc);
+    const R t1 = (tc - root) * rdd, t2 = (tc + root) * rdd;
+    if constexpr (kNearest) {
+        emit(sel(t1 >= (R)0, t1, t2), v);
+    } else {
+        emit(t1, v);
+        emit(t2, v);
+    }
+}
+template <typename R, int K>
+__device__ inline bool world_sphere(const ShapeRec<R>& s) {
+    if constexpr (sizeof(R) == 4 && K == RT_SHAPE_SPHERE) return (s.flags & kShapeSimilar) != 0;
+    return false;
+}
+template <typename R>
+__device__ inline R recip(R x) {
+    if constexpr (sizeof(R) == 4) return __builtin_amdgcn_rcpf(x);
+    else return (R)1 / x;
+}
+
 // Wave-level cull (acceleration only): false when no active lane's ray
 // o + t d, t >= 0, can meet the shape's padded world bounding sphere
 // (rtc_host.cpp bounding_sphere), so the wave skips the shape; the reference
@@ -752,15 +788,19 @@ __device__ inline bool skips_on(const DevScene<R>& sc) {
 template <typename R>
 __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
     Nearest<R> best;
-    const R dd = dot(d, d);
+    const R dd = dot(d, d), rdd = recip(dd);
     for_all_culled<R, true>(sc, o, d, dd, [&]<int K>(const ShapeRec<R>& s, int slot) {
         jit_fence(o, d, slot);
         if (!wave_may_hit<R, K>(s, o, d, dd)) return;
-        const V3<R> lo = xform_point(s.inv, o);
-        const V3<R> ld = xform_vector(s.inv, d);
         // (per-scene records: the slot rides below the world index; world
         // indices are distinct, so the order is the world order)
         const int w = kJitRecords && sizeof(R) == 4 ? (s.world_index << 8) | slot : s.world_index;
+        if (world_sphere<R, K>(s)) {
+            sphere_world<R, true>(s, o, d, dd, rdd, [&](R t, bool v) { best.offer(t, v, w); });
+            return;
+        }
+        const V3<R> lo = xform_point(s.inv, o);
+        const V3<R> ld = xform_vector(s.inv, d);
         if constexpr (K == RT_SHAPE_CUBE && sizeof(R) == 4) {
             // A wave whose every origin lies strictly inside an enclosing cube:
             // each slab's entry is then negative and its exit positive, so the
@@ -818,7 +858,7 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist, 
     return false;
 #endif
     Blocker<R> b;
-    const R dd = dot(d, d);
+    const R dd = dot(d, d), rdd = recip(dd);
     // once every active lane is blocked the remaining clusters cannot change
     // the answer (per cluster, not per shape: a per-shape check measured
     // slower in round 3; per cluster cover -2.5 %, cylinders -4 %, table +1 %)
@@ -854,6 +894,10 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist, 
             if (!wave_any(!clear)) return;
         }
         if (!wave_may_hit<R, K>(s, o, d, dd)) return;
+        if (world_sphere<R, K>(s)) {
+            sphere_world<R, false>(s, o, d, dd, rdd, [&](R t, bool v) { b.offer(t, v, dist); });
+            return;
+        }
         const V3<R> lo = xform_point(s.inv, o);
         if (K == RT_SHAPE_PLANE && skips) {
             // A plane blocks the segment from o to the light only if they lie on
@@ -930,18 +974,22 @@ __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> 
     // entries of one shape before the hit: their count and the latest
     auto scan = [&]<int K>(const ShapeRec<R>& s, int& count, Key& last) {
         jit_fence(o, d);
-        const V3<R> lo = xform_point(s.inv, o);
-        const V3<R> ld = xform_vector(s.inv, d);
         const int w = s.world_index;
         int e = 0;
-        entries<R, K>(s, lo, ld, [&](R t, bool v) {
+        auto take = [&](R t, bool v) {
             const Key k{t, w, e};
             if (v && before(k, hk)) {
                 ++count;
                 if (count == 1 || before(last, k)) last = k;
             }
             e += v ? 1 : 0;
-        });
+        };
+        if (world_sphere<R, K>(s)) {  // (the same roots as closest_hit's)
+            const R dd = dot(d, d);
+            sphere_world<R, false>(s, o, d, dd, recip(dd), take);
+            return;
+        }
+        entries<R, K>(s, xform_point(s.inv, o), xform_vector(s.inv, d), take);
     };
 #if defined(RTC_JIT) && !defined(RTC_NO_WALK_CULL)
     // worlds of a few bounded shapes (refraction.yaml: a lens of two spheres
@@ -2707,6 +2755,16 @@ __global__ void debug_shape(const ShapeRec<R>* __restrict__ shapes, int slot, in
     if (mode == 0) {
         const double* q = in + 6 * (size_t)i;
         V3<R> o = {(R)q[0], (R)q[1], (R)q[2]}, d = {(R)q[3], (R)q[4], (R)q[5]};
+        double* r0 = out + (1 + kDebugMaxEntries) * (size_t)i;
+        if (world_space && kind == RT_SHAPE_SPHERE && world_sphere<R, RT_SHAPE_SPHERE>(s)) {  // the tracers' own test
+            int c = 0;
+            const R dd = dot(d, d);
+            sphere_world<R, false>(s, o, d, dd, recip(dd), [&](R t, bool v) {
+                if (v && c < kDebugMaxEntries) r0[1 + c++] = (double)t;
+            });
+            r0[0] = (double)c;
+            return;
+        }
         if (world_space) {
             const V3<R> lo = xform_point(s.inv, o), ld = xform_vector(s.inv, d);
             o = lo;
