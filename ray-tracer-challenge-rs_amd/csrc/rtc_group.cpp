@@ -133,22 +133,25 @@ int render_shards(rt_context* ctx, const rt_camera_desc* cam, const rt_render_op
     const uint32_t rows = tile_rows_for(cam->height, G, 0) * RT_TILE_H;  // shard 0 has the most rows
     const size_t strip = (size_t)rows * cam->width * pixel_bytes(o);
     int rc;
+    auto stream_of = [&](rt_context* m) { return m->rank == 0 ? root_stream : m->stream; };
     for (rt_context* m : ms) {
         RT_HIP(hipSetDevice(m->device));
-        if ((rc = ensure(&m->d_strip, &m->strip_bytes, strip))) return rc;
+        if (m->rank != 0 && (rc = ensure(&m->d_strip, &m->strip_bytes, strip))) return rc;
         if (m->rank == 0 && (rc = ensure(&m->d_gathered, &m->gathered_bytes, strip * G))) return rc;
     }
-    auto stream_of = [&](rt_context* m) { return m->rank == 0 ? root_stream : m->stream; };
+    // Rank 0 renders its strip straight into its slot of the gather buffer
+    // (slot 0), and gathers in place: RCCL then copies only the other ranks'.
+    auto strip_of = [&](rt_context* m) { return m->rank == 0 ? m->d_gathered : m->d_strip; };
     for (rt_context* m : ms) {
         hipStream_t s = stream_of(m);
         RT_HIP(hipSetDevice(m->device));
         if (timed) RT_HIP(hipEventRecord(m->ev_render0, s));
-        if ((rc = launch_frame(m, cam, o, (uint32_t)m->rank, G, m->d_strip, s))) return rc;
+        if ((rc = launch_frame(m, cam, o, (uint32_t)m->rank, G, strip_of(m), s))) return rc;
         if (timed) RT_HIP(hipEventRecord(m->ev_render1, s));
     }
     RT_NCCL(ncclGroupStart());
     for (rt_context* m : ms)
-        RT_NCCL(ncclGather(m->d_strip, m->rank == 0 ? m->d_gathered : nullptr, strip, ncclUint8, 0, m->comm,
+        RT_NCCL(ncclGather(strip_of(m), m->rank == 0 ? m->d_gathered : nullptr, strip, ncclUint8, 0, m->comm,
                            stream_of(m)));
     RT_NCCL(ncclGroupEnd());
     for (rt_context* m : ms) {

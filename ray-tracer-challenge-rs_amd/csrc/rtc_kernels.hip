@@ -2729,8 +2729,19 @@ __global__ void assemble_shards(const unsigned char* __restrict__ gathered, unsi
     const uint64_t src_row = (uint64_t)shard * strip_rows + strip_row;
     const unsigned char* src = gathered + src_row * row_bytes;
     unsigned char* dst = image + (uint64_t)y * row_bytes;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < row_bytes; i += (uint64_t)gridDim.x * blockDim.x)
-        dst[i] = src[i];
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    if (((row_bytes | (uintptr_t)gathered | (uintptr_t)image) & 15) == 0) {
+        // 16-byte rows (every width of an f32/f64 canvas, u8 ones of width
+        // % 16 == 0: a 4K u8 frame): one dwordx4 per thread instead of 16
+        // byte accesses (round 5: the 1-rank tiled cover 4K frame's gather +
+        // de-interleave 62 -> 11 us with rank 0's in-place gather, rtc_group.cpp)
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+        uint4* d4 = reinterpret_cast<uint4*>(dst);
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < row_bytes / 16; i += stride)
+            d4[i] = s4[i];
+        return;
+    }
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < row_bytes; i += stride) dst[i] = src[i];
 }
 #endif  // helper kernels
 #ifndef RTC_JIT
@@ -2901,7 +2912,10 @@ hipError_t launch_canvas_wait(const unsigned long long* flags, uint32_t n, unsig
 hipError_t launch_assemble(const void* gathered, void* image, uint32_t width, uint32_t height, uint32_t shards,
                            uint32_t strip_rows, uint32_t bpp, hipStream_t stream) {
     (void)hipGetLastError();  // see launch_trace
-    dim3 grid(4, height);
+    const uint64_t row_bytes = (uint64_t)width * bpp;
+    const bool wide = ((row_bytes | (uintptr_t)gathered | (uintptr_t)image) & 15) == 0;
+    const uint64_t per_row = wide ? (row_bytes / 16 + 255) / 256 : 4;  // blocks per row (kernel's two paths)
+    dim3 grid((uint32_t)std::min<uint64_t>(std::max<uint64_t>(per_row, 1), 64), height);
     hipLaunchKernelGGL(assemble_shards, grid, dim3(256), 0, stream, static_cast<const unsigned char*>(gathered),
                        static_cast<unsigned char*>(image), width, height, shards, strip_rows, bpp);
     return hipGetLastError();
