@@ -174,6 +174,33 @@ bool similar_sphere(const rt_shape_desc& d, double centre[3], double* r2) {
     return true;
 }
 
+// A cube whose transformation has a diagonal linear part (rtc_internal.hpp
+// kShapeAxisAligned): per axis the world coordinates of its object -1 and +1
+// faces, the world |d| below which the axis counts as parallel (EPSILON over
+// the axis's scale: the object direction is s d) and the scale's sign, for
+// the f32 kernels' world-space slab test.  Off-diagonal terms within 1e-12 of
+// the diagonal's size count as zero (far below f32 rounding).
+bool axis_aligned_cube(const rt_shape_desc& d, double face_lo[3], double face_hi[3], double eps[3], double sgn[3]) {
+    if (d.kind != RT_SHAPE_CUBE) return false;
+    const double* m = d.inverse;  // rows of the inverse (row-major 4x4)
+    if (m[12] != 0.0 || m[13] != 0.0 || m[14] != 0.0 || m[15] != 1.0) return false;
+    double dmax = 0.0;
+    for (int i = 0; i < 3; ++i) dmax = std::max(dmax, std::fabs(m[4 * i + i]));
+    if (!(dmax > 0.0) || !std::isfinite(dmax)) return false;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            if (i != j && !(std::fabs(m[4 * i + j]) <= 1e-12 * dmax)) return false;
+    for (int i = 0; i < 3; ++i) {
+        const double sc = m[4 * i + i], t = m[4 * i + 3];
+        if (sc == 0.0 || !std::isfinite(sc) || !std::isfinite(t)) return false;
+        face_lo[i] = (-1.0 - t) / sc;
+        face_hi[i] = (1.0 - t) / sc;
+        eps[i] = 0.00000008 / std::fabs(sc);  // consts.rs EPSILON
+        sgn[i] = sc > 0.0 ? 1.0 : -1.0;
+    }
+    return true;
+}
+
 // Device table order: by kind, then by identity class (the world index of
 // the class's first shape), then by world index.  Without value-equal shapes
 // this is world order within each kind.  The tie rule never depends on the
@@ -227,10 +254,19 @@ int build_world(rt_context* ctx, DeviceWorld<R>& w, const rt_shape_desc* shapes,
                 for (int q = 0; q < 3; ++q) r.tri[q] = (R)centre[q];
                 r.tri[3] = (R)r2;
             }
+            double flo[3], fhi[3], feps[3], fsgn[3];
+            const bool aligned = axis_aligned_cube(d, flo, fhi, feps, fsgn);
+            if (aligned)
+                for (int q = 0; q < 3; ++q) {
+                    r.tri[q] = (R)flo[q];
+                    r.tri[3 + q] = (R)fhi[q];
+                    r.tri[6 + q] = (R)feps[q];
+                    r.tri[9 + q] = (R)fsgn[q];
+                }
             r.world_index = (int32_t)i;
             r.material = d.material;
             const bool class_end = next + 1 >= order.size() || cls[order[next + 1]] != cls[i];
-            r.flags = (d.closed ? kShapeClosed : 0) | (class_end ? kShapeClassEnd : 0) | (similar ? kShapeSimilar : 0) |
+            r.flags = (d.closed ? kShapeClosed : 0) | (class_end ? kShapeClassEnd : 0) | (similar ? kShapeSimilar : 0) | (aligned ? kShapeAxisAligned : 0) |
                       (int32_t)(cls[i] << kShapeClassShift);
             r.casts_shadow = mats[d.material].casts_shadow ? 1 : 0;
             sh.push_back(r);

@@ -218,6 +218,13 @@ constexpr int32_t kShapeClassEnd = 2;  // last member of its identity class
 // centre and tri[3] its radius^2, and the f32 kernels find its roots in world
 // space (rtc_kernels.hip sphere_world).
 constexpr int32_t kShapeSimilar = 4;
+// A cube whose transformation has a diagonal linear part (scale and
+// translation only: rtc_host.cpp axis_aligned_cube): tri[0..2] holds the
+// world coordinates of its object -1 faces, tri[3..5] of its +1 faces,
+// tri[6..8] the world |d| below which an axis counts as parallel (EPSILON
+// over the axis's scale) and tri[9..11] the scale's signs, and the f32
+// kernels run its slab test in world space (rtc_kernels.hip cube_world).
+constexpr int32_t kShapeAxisAligned = 8;
 constexpr int kShapeClassShift = 8;
 
 template <typename R>
@@ -234,7 +241,8 @@ struct alignas(16) ShapeRec {
     int32_t flags;  // kShapeClosed | kShapeClassEnd | identity class << kShapeClassShift
     R ymin, ymax;  // cylinder/cone min/max (cylinder.rs:12-14)
     R tri[12];     // triangle vertex_1, edge_1, edge_2, normal (triangle.rs:12-17);
-                   // a kShapeSimilar sphere: world centre, radius^2
+                   // a kShapeSimilar sphere: world centre, radius^2;
+                   // a kShapeAxisAligned cube: its world slabs
 };
 
 template <typename R>
