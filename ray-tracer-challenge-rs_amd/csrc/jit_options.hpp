@@ -14,8 +14,13 @@ inline std::vector<std::string> jit_kind_defines(bool pool, bool no_skips) {
     // tests in between may interleave (more ILP) and still fit 8 waves/SIMD
     // without spilling.  Same-box A/B against a fence per shape: shadow_puppets
     // -3.6 %, three_sphere 4K -2.5 %, 1080p -0.6 %; the pool kernel lost 15 %
-    // on cover that way and keeps a fence per shape.
-    if (!pool) d.push_back("-DRTC_JIT_FENCE_EVERY=3");
+    // on cover that way and keeps a fence per shape.  Worlds of at most 8
+    // shapes take no fence (round 5, same box: three_sphere 15.48 -> 15.31 us,
+    // shadow_puppets 19.69 -> 18.90 us; 36 VGPRs, no spills).
+    if (!pool) {
+        d.push_back("-DRTC_JIT_FENCE_EVERY=3");
+        d.push_back("-DRTC_JIT_FENCE_MIN_SHAPES=9");
+    }
     // Shape records as constants (rtc_kernels.hip kJitRecords) pay off in the
     // direct kernel only.  Same-box A/B, two rounds (profiles/ab/r04_ab_builds.log):
     // direct three_sphere 17.0 us with them vs 18.4 us without; pool kernels

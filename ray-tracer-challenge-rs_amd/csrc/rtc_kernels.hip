@@ -638,10 +638,15 @@ __device__ inline bool wave_line_may_hit(const ShapeRec<R>& s, V3<R> o, V3<R> d,
 #ifndef RTC_JIT_FENCE_EVERY
 #define RTC_JIT_FENCE_EVERY 1
 #endif
+// Worlds of fewer shapes than this take no fence at all (the direct kernel's
+// builds: rtc_jit.cpp; the pool kernel's default 0 fences every world).
+#ifndef RTC_JIT_FENCE_MIN_SHAPES
+#define RTC_JIT_FENCE_MIN_SHAPES 0
+#endif
 template <typename R>
 __device__ inline void jit_fence(V3<R>& o, V3<R>& d, int slot = 0) {
 #if defined(RTC_JIT) && !defined(RTC_JIT_NO_FENCE)
-    if constexpr (sizeof(R) == 4)
+    if constexpr (sizeof(R) == 4 && jit::kBegin[kNumKinds] >= RTC_JIT_FENCE_MIN_SHAPES)
         if (slot % RTC_JIT_FENCE_EVERY == 0)
             asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z), "+v"(d.x), "+v"(d.y), "+v"(d.z));
 #endif

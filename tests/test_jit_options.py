@@ -39,5 +39,6 @@ def test_kind_defines(tmp_path):
     for ns in (False, True):
         direct, pool = rows[(False, ns)], rows[(True, ns)]
         assert "-DRTC_JIT_NO_RECORDS" not in direct and "-DRTC_JIT_FENCE_EVERY=3" in direct
+        assert "-DRTC_JIT_FENCE_MIN_SHAPES=9" in direct
         assert "-DRTC_JIT_NO_RECORDS" in pool and not any(d.startswith("-DRTC_JIT_FENCE_EVERY") for d in pool)
         assert ("-DRTC_NO_SKIPS" in direct) == ns and ("-DRTC_NO_SKIPS" in pool) == ns
