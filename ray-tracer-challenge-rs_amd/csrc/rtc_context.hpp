@@ -158,11 +158,12 @@ struct rt_context {
     uint32_t jit_pattern_kinds = ~0u;              // pattern kinds in the world's table (bit per RT_PATTERN_*)
     bool jit_transparent = true;                   // some material is transparent (else no refraction code)
     int32_t jit_begin[rtc::kNumKinds + 1] = {};
-    // variants: pool x LDS world x RT_FLAG_NO_SKIPS (rtc_jit.cpp jit_function)
-    hipFunction_t jit_fn[8] = {};
-    std::shared_ptr<rtc::CodeBuild> jit_build[8];  // the build each variant waits for (host thread)
-    bool jit_rejected[8] = {};   // built, but refused for occupancy or scratch (that variant only)
-    bool jit_owner[8] = {};      // this context started the build: its time goes into jit_compile_ms
+    // variants: pool x LDS world x RT_FLAG_NO_SKIPS x (pool) 7 waves/SIMD (rtc_jit.cpp jit_function)
+    static constexpr int kJitVariants = 16;
+    hipFunction_t jit_fn[kJitVariants] = {};
+    std::shared_ptr<rtc::CodeBuild> jit_build[kJitVariants];  // the build each variant waits for (host thread)
+    bool jit_rejected[kJitVariants] = {};   // built, but refused for occupancy or scratch (that variant only)
+    bool jit_owner[kJitVariants] = {};      // this context started the build: its time goes into jit_compile_ms
     uint32_t jit_frames = 0;     // large f32 frames of this upload so far (RT_JIT_AUTO starts at the 2nd)
     std::string arch;            // the device's gfx target (gcnArchName), for hipRTC; read lazily (device_arch)
     int jit_mode = 2;
@@ -252,8 +253,10 @@ unsigned long long timeout_ticks(double timeout_ms);
 // rtc_jit.cpp: the per-scene kernel of this context's world for a launch of
 // `static_blocks` workgroups per CU, or null (use the generic kernel)
 constexpr uint32_t kJitMinTiles = 256;  // 64K pixels
+// *pool_waves: the waves/SIMD the returned pool kernel was built for (7, or
+// 6 = the static build's), so the caller can plan its LDS for them.
 int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int static_blocks, hipFunction_t* fn,
-                 bool no_skips = false);
+                 bool no_skips = false, int* pool_waves = nullptr);
 int jit_wait(rt_context* ctx, double timeout_ms, int* pending);
 const std::string& device_arch(rt_context* ctx);  // rtc_jit.cpp: the device's gfx target, read once
 

@@ -457,6 +457,7 @@ struct LaunchShape {
     uint32_t grid;
     size_t lds;
     uint32_t cap, lcap, batch;  // pool: LIFO bound, its LDS-resident part, pop batch
+    uint32_t grid_tiles;        // the launch's tiles (the grid's upper bound)
 };
 
 // Cached occupancy (workgroups per CU) of one kernel instantiation at a
@@ -524,6 +525,47 @@ constexpr int32_t kJitRecordsMaxShapes = 255;
 constexpr int32_t kJitRecordsMaxShapes = -1;
 #endif
 
+// A per-scene pool kernel built for more waves/SIMD than the static one
+// (rtc_jit.cpp jit_function): the pool's LDS share re-planned for the
+// workgroups per CU its registers allow, as pool_lds_rays does for the
+// static kernel, and the resident grid with it.
+template <typename R>
+int plan_pool_for(rt_context* ctx, hipFunction_t fn, LaunchShape& ls) {
+    constexpr uint32_t kMinRays = kBlock;
+    auto blocks = [&](size_t lds, int* per_cu) -> int {
+        int api = 0;
+        RT_HIP(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&api, fn, kBlock, lds));
+        const size_t per_block = (kStaticLds + lds + 511) / 512 * 512;
+        *per_cu = std::min(api, (int)((size_t)kLdsPerCu / per_block));
+        return RT_OK;
+    };
+    int best = 0, rc;
+    if ((rc = blocks(ls.world_lds + pool_lds_bytes<R>(kMinRays), &best))) return rc;
+    if (best <= ls.per_cu) return RT_OK;  // no more workgroups than planned: keep the plan
+    const size_t rec = 7 * sizeof(R) + sizeof(PoolMeta);
+    const size_t budget = (size_t)kLdsPerCu / (size_t)best;
+    const size_t fixed = kStaticLds + ls.world_lds + pool_lds_bytes<R>(0) + 511;
+    uint32_t n = budget > fixed ? (uint32_t)((budget - fixed) / rec) : kMinRays;
+    const size_t room = ctx->lds_per_block > fixed ? ctx->lds_per_block - fixed : 0;
+    n = std::min<uint32_t>(n, (uint32_t)(room / rec));
+    n = std::min<uint32_t>(ls.cap, std::max<uint32_t>(kMinRays, n & ~7u));
+    for (;;) {
+        int got = 0;
+        if ((rc = blocks(ls.world_lds + pool_lds_bytes<R>(n), &got))) return rc;
+        if (got >= best || n <= kMinRays) break;
+        n = std::max<uint32_t>(kMinRays, n - 8);
+    }
+    int got = 0;
+    if ((rc = blocks(ls.world_lds + pool_lds_bytes<R>(n), &got))) return rc;
+    if (got <= ls.per_cu) return RT_OK;
+    ls.lcap = n;
+    ls.lds = ls.world_lds + pool_lds_bytes<R>(n);
+    ls.per_cu = got;
+    const uint64_t resident = (uint64_t)got * (uint64_t)ctx->cu_count;
+    ls.grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ls.grid_tiles, resident));
+    return RT_OK;
+}
+
 template <typename R>
 int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t n_tiles, LaunchShape& ls,
                 bool jit_records = false) {
@@ -559,6 +601,7 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
     const bool oversub = !ls.pool && ls.sched == kSchedStatic && sizeof(R) == 4;
     const uint64_t grid_cap = oversub ? resident * 5 / 2 : resident;
     ls.grid = ls.sched != kSchedGrid ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, grid_cap)) : n_tiles;
+    ls.grid_tiles = n_tiles;
     return RT_OK;
 }
 
@@ -728,9 +771,11 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
             if (ctx->lds_world && !ls.pool && w.scene.kind_begin[kNumKinds] <= kJitRecordsMaxShapes &&
                 (rc = plan_launch<R>(ctx, w.scene, depth, P.n_tiles, lj, true)))
                 return rc;
+            int waves = 0;
             if ((rc = jit_function(ctx, lj.pool, lj.world_lds != 0, lj.lds, lj.per_cu, &jf,
-                                   (flags & RT_FLAG_NO_SKIPS) != 0)))
+                                   (flags & RT_FLAG_NO_SKIPS) != 0, &waves)))
                 return rc;
+            if (jf && waves > 0 && (rc = plan_pool_for<R>(ctx, jf, lj))) return rc;
             if (jf) ls = lj;
         }
     }
@@ -1227,7 +1272,7 @@ int capture_jit_table(rt_context* ctx) {
     ctx->jit_pattern_kinds = 0;
     for (const PatternRec<float>& q : ctx->jit_pattern_recs)  // every kind a pattern_color walk can meet (complex sub-patterns included)
         ctx->jit_pattern_kinds |= 1u << std::min<uint32_t>((uint32_t)q.kind, RT_PATTERN_TEST);
-    for (int v = 0; v < 8; ++v) {
+    for (int v = 0; v < rt_context::kJitVariants; ++v) {
         ctx->jit_fn[v] = nullptr;
         ctx->jit_build[v].reset();
         ctx->jit_rejected[v] = ctx->jit_owner[v] = false;

@@ -385,7 +385,7 @@ std::vector<std::string> build_defines() {
 
 // Everything the compiler sees for one build, and the key naming it.
 jitfile::Request make_request(const std::string& scene, const char* name, const std::string& arch, uint64_t* key,
-                              bool no_skips) {
+                              bool no_skips, int pool_waves) {
     jitfile::Request rq;
     rq.name = name;
     rq.main_src = std::string("#define RTC_JIT 1\n#include \"rtc_jit_scene.hpp\"\n") + kSrcKernels;
@@ -404,7 +404,7 @@ jitfile::Request make_request(const std::string& scene, const char* name, const 
     static const std::vector<std::string> defines = build_defines();
     rq.opts.insert(rq.opts.end(), defines.begin(), defines.end());
     // per kind: fence spacing, records as constants, the no-skips build
-    const auto kind = jit_kind_defines(std::strstr(name, "pool") != nullptr, no_skips);
+    const auto kind = jit_kind_defines(std::strstr(name, "pool") != nullptr, no_skips, pool_waves);
     rq.opts.insert(rq.opts.end(), kind.begin(), kind.end());
     // RTC_DEBUG=jit_flags=...: extra compiler options, space-separated (A/B diagnostics)
     if (std::string all; debug_knob("jit_flags", &all)) {
@@ -572,11 +572,14 @@ const std::string& device_arch(rt_context* ctx) {
 // generic kernel this launch).  RT_JIT_SYNC builds in line; RT_JIT_AUTO /
 // RT_JIT_EAGER start the build at the 2nd / 1st large frame of an upload and
 // return null until it has landed.
-int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int static_blocks, hipFunction_t* fn,
-                 bool no_skips) {
+namespace {
+// One variant's build: *fn stays null while it compiles, if it failed or if
+// it was refused (jit_rejected[variant]).
+// start_only: make sure the build runs (in the background even in
+// RT_JIT_SYNC mode) and return without waiting for it or taking it.
+int jit_variant(rt_context* ctx, int variant, bool pool, bool lds, size_t dyn_lds, int static_blocks,
+                hipFunction_t* fn, bool no_skips, int pool_waves, bool start_only = false) {
     *fn = nullptr;
-    if (ctx->jit_failed || ctx->jit_shapes.empty()) return RT_OK;
-    const int variant = (no_skips ? 4 : 0) + (pool ? 2 : 0) + (lds ? 1 : 0);
     if (ctx->jit_fn[variant]) {
         *fn = ctx->jit_fn[variant];
         return RT_OK;
@@ -616,10 +619,11 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
                 make_request(scene_header(ctx->jit_shapes, ctx->jit_begin, ctx->jit_lights, ctx->jit_materials,
                                           ctx->jit_patterns,
                                           ctx->jit_pattern_kinds, ctx->jit_transparent),
-                             kernel_name(pool, lds), device_arch(ctx), &key, no_skips);
-            start_build(b, rq, key, sync);
+                             kernel_name(pool, lds), device_arch(ctx), &key, no_skips, pool_waves);
+            start_build(b, rq, key, sync && !start_only);
         }
     }
+    if (start_only) return RT_OK;
     if (sync) {  // a build another context started: wait for it
         std::unique_lock<std::mutex> lk(g_mu);
         g_cv.wait(lk, [&] { return b->state.load() != 0; });
@@ -687,6 +691,34 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
     ctx->jit_fn[variant] = mf.second;
     *fn = mf.second;
     return RT_OK;
+}
+}  // namespace
+
+int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int static_blocks, hipFunction_t* fn,
+                 bool no_skips, int* pool_waves) {
+    *fn = nullptr;
+    if (pool_waves) *pool_waves = 0;
+    if (ctx->jit_failed || ctx->jit_shapes.empty()) return RT_OK;
+    const int variant = (no_skips ? 4 : 0) + (pool ? 2 : 0) + (lds ? 1 : 0);
+    if (!pool) return jit_variant(ctx, variant, pool, lds, dyn_lds, static_blocks, fn, no_skips, 0);
+    // The pool kernel at 7 waves/SIMD (jit_options.hpp) and, compiled beside
+    // it, at the static build's occupancy: a 7-wave build that spills more
+    // than 16 B/lane is refused and the other is taken (also while the
+    // 7-wave one still compiles).  Both land in the disk cache, so a later
+    // process has its kernel at the first frame either way.  The 7-wave
+    // build is checked against the static plan's LDS (it passes at 6
+    // workgroups/CU) and the caller re-plans the pool's LDS for 7
+    // (rtc_host.cpp plan_pool_for).
+    int rc = jit_variant(ctx, variant, pool, lds, dyn_lds, static_blocks, fn, no_skips, 0, true);
+    if (rc) return rc;
+    rc = jit_variant(ctx, variant + 8, pool, lds, dyn_lds, static_blocks, fn, no_skips, 7);
+    if (rc || ctx->jit_failed) return rc;
+    if (*fn) {
+        if (pool_waves) *pool_waves = 7;
+        return RT_OK;
+    }
+    // (0 waves: the static build's occupancy, as planned)
+    return jit_variant(ctx, variant, pool, lds, dyn_lds, static_blocks, fn, no_skips, 0);
 }
 
 // Block until this context's builds in flight have finished (rt_jit_wait).

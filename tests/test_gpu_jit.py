@@ -226,10 +226,14 @@ def test_exit_with_a_build_in_flight(tmp_path):
 
     first = run(3)  # RT_JIT_EAGER: the build starts at this frame, the process exits at once
     assert not first["used"]
-    deadline = time.time() + 60
-    while time.time() < deadline and not (cache.exists() and any(p.suffix == ".co" for p in cache.iterdir())):
+    # (a pool world compiles two builds, at 7 waves/SIMD and at the static
+    # occupancy: rtc_jit.cpp jit_function; both must land)
+    deadline = time.time() + 90
+    def landed():
+        return sum(p.suffix == ".co" for p in cache.iterdir()) if cache.exists() else 0
+    while time.time() < deadline and landed() < 2:
         time.sleep(0.2)
-    assert any(p.suffix == ".co" for p in cache.iterdir()), "the orphaned compile did not land in the cache"
+    assert landed() >= 2, "the orphaned compiles did not land in the cache"
     second = run(3)  # the build comes from the disk cache at the first frame
     assert second["used"] and second["rays"] == first["rays"]
     assert second["ms"] < 100, second

@@ -23,6 +23,11 @@ int main() {
             for (const auto& d : rtc::jit_kind_defines(pool, ns)) std::printf(" %s", d.c_str());
             std::printf("\n");
         }
+    std::printf("w7");  // the pool kernel's 7-wave attempt (rtc_jit.cpp jit_function)
+    for (const auto& d : rtc::jit_kind_defines(true, false, 7)) std::printf(" %s", d.c_str());
+    std::printf("\nw7direct");
+    for (const auto& d : rtc::jit_kind_defines(false, false, 7)) std::printf(" %s", d.c_str());
+    std::printf("\n");
 }
 """
 
@@ -32,10 +37,16 @@ def test_kind_defines(tmp_path):
     src.write_text(PROG)
     exe = tmp_path / "opts"
     subprocess.run(["g++", "-std=c++17", "-O0", "-I", CSRC, "-o", str(exe), str(src)], check=True)
-    rows = {}
+    rows, extra = {}, {}
     for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        if line.startswith("w7"):
+            tag, *defs = line.split()
+            extra[tag] = set(defs)
+            continue
         pool, ns, *defs = line.split()
         rows[(pool == "1", ns == "1")] = set(defs)
+    assert "-DRTC_POOL_WAVES=7" in extra["w7"] and "-DRTC_JIT_NO_RECORDS" in extra["w7"]
+    assert not any(d.startswith("-DRTC_POOL_WAVES") for d in extra["w7direct"])  # the direct kernel ignores it
     for ns in (False, True):
         direct, pool = rows[(False, ns)], rows[(True, ns)]
         assert "-DRTC_JIT_NO_RECORDS" not in direct and "-DRTC_JIT_FENCE_EVERY=3" in direct
