@@ -265,3 +265,42 @@ def test_device_render_default_world_pixel(gpu_ctx, rtc):
     assert np.abs(img[5, 5] - exp).max() < EPSILON
     img32, _ = gpu_ctx.render(cam, 6, precision="f32")
     assert np.abs(img32[5, 5] - exp).max() < 1e-5
+
+
+def test_world_space_sphere_and_cube_tests_agree_with_object_space(gpu_ctx):
+    """f32 spheres whose transformation is a similarity and axis-aligned cubes
+    run their tests in world space (rtc_kernels.hip sphere_world / cube_world,
+    round 5); the f64 path keeps the reference's object-space arithmetic
+    (sphere.rs:41-53, cube.rs:22-85).  On random rays through each such shape
+    (and an ellipsoid and a rotated cube, which keep the object-space test in
+    f32 too) the f32 entries match the f64 ones in number for all but rays
+    grazing an edge, and in value to f32 rounding."""
+    from rtc_amd import world as W
+    shapes = [
+        W.sphere(transform=W.mat_mul(W.translation(1.5, -0.5, 2.0), W.scaling(0.7, 0.7, 0.7))),
+        W.sphere(transform=W.mat_mul(W.translation(-2, 1, 0), W.mat_mul(W.rotation_y(0.7), W.scaling(1.3, 1.3, 1.3)))),
+        W.sphere(transform=W.mat_mul(W.translation(0, 2, -1), W.scaling(1.0, 0.4, 1.0))),  # ellipsoid
+        W.cube(transform=W.mat_mul(W.translation(0.5, -1, 1), W.scaling(2.0, 0.3, 1.1))),
+        W.cube(transform=W.mat_mul(W.translation(-1, 0, -2), W.scaling(-0.8, 1.5, 0.6))),  # a mirrored axis
+        W.cube(transform=W.mat_mul(W.translation(2, 1, -2), W.rotation_y(0.4))),
+    ]
+    gpu_ctx.upload(W.World([W.Light((-10, 10, -10))], shapes).tables())
+    rng = np.random.default_rng(5)
+    n = 4096
+    o = rng.uniform(-6, 6, size=(n, 3))
+    centres = [(1.5, -0.5, 2.0), (-2, 1, 0), (0, 2, -1), (0.5, -1, 1), (-1, 0, -2), (2, 1, -2)]
+    for idx in range(len(shapes)):
+        # aim at the shape's neighbourhood so most rays hit
+        target = np.array(centres[idx]) + rng.uniform(-1.2, 1.2, size=(n, 3))
+        d = target - o
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        rays = np.concatenate([o, d], axis=1)
+        a = gpu_ctx.debug_intersect(idx, rays, precision="f64", world_space=True)
+        b = gpu_ctx.debug_intersect(idx, rays, precision="f32", world_space=True)
+        same = [i for i in range(n) if len(a[i]) == len(b[i])]
+        assert len(same) >= 0.995 * n, (idx, len(same))
+        hits = [i for i in same if a[i]]
+        assert len(hits) > n // 5, (idx, len(hits))  # the rays do meet the shape
+        err = np.array([abs(x - y) / max(1.0, abs(x)) for i in hits for x, y in zip(a[i], b[i])])
+        # (near-tangent rays: the roots' split is a square root of a rounding-sized discriminant)
+        assert np.percentile(err, 99) < 1e-4 and err.max() < 5e-2, (idx, np.percentile(err, 99), err.max())
