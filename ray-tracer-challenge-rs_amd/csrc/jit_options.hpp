@@ -9,10 +9,10 @@
 namespace rtc {
 
 // pool_waves: the pool kernel's waves per SIMD (RTC_POOL_WAVES), 0 = the
-// static build's.  rtc_jit.cpp tries 7 first and keeps a build at that
-// occupancy when it spills at most 16 B/lane (round 5, same box against 6:
-// table 4K -4.0 %, refraction -2.7 %, reflect_refract -1.2 %); cover's
-// build spills 44 B/lane at 7 and falls back to a build at 6.
+// static build's.  rtc_jit.cpp compiles 7 beside the static occupancy and
+// keeps the 7-wave build when it spills at most kPool7ScratchMax (round 5,
+// same box against 6: table 4K -3.6 %, cover 4K -4.3 %, reflect_refract
+// -2.4 %); cylinders' build spills 44 B/lane at 7 and takes the other.
 inline std::vector<std::string> jit_kind_defines(bool pool, bool no_skips, int pool_waves = 0) {
     std::vector<std::string> d;
     if (pool && pool_waves > 0) d.push_back("-DRTC_POOL_WAVES=" + std::to_string(pool_waves));

@@ -572,13 +572,20 @@ const std::string& device_arch(rt_context* ctx) {
 // generic kernel this launch).  RT_JIT_SYNC builds in line; RT_JIT_AUTO /
 // RT_JIT_EAGER start the build at the 2nd / 1st large frame of an upload and
 // return null until it has landed.
+// Scratch a 7-wave per-scene pool build may use (B/lane): the workgroup
+// it gains outweighs up to this much spilling.  Same box, 7-wave build vs
+// the 6-wave one: cover 4K (36 B/lane) 0.657 -> 0.629 ms, reflect_refract
+// and table (16) -2.4 % / -3.6 %; cylinders (44) +4 % (refused).
+constexpr int kPool7ScratchMax = 40;
+
 namespace {
 // One variant's build: *fn stays null while it compiles, if it failed or if
 // it was refused (jit_rejected[variant]).
 // start_only: make sure the build runs (in the background even in
 // RT_JIT_SYNC mode) and return without waiting for it or taking it.
+// scratch_max: the B/lane of scratch a pool build may use (direct: none).
 int jit_variant(rt_context* ctx, int variant, bool pool, bool lds, size_t dyn_lds, int static_blocks,
-                hipFunction_t* fn, bool no_skips, int pool_waves, bool start_only = false) {
+                hipFunction_t* fn, bool no_skips, int pool_waves, int scratch_max, bool start_only = false) {
     *fn = nullptr;
     if (ctx->jit_fn[variant]) {
         *fn = ctx->jit_fn[variant];
@@ -681,7 +688,7 @@ int jit_variant(rt_context* ctx, int variant, bool pool, bool lds, size_t dyn_ld
     int blocks = 0, scratch = 0;
     RT_HIP(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mf.second, kBlock, dyn_lds));
     RT_HIP(hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, mf.second));
-    if (blocks < static_blocks || scratch > (pool ? 16 : 0)) {
+    if (blocks < static_blocks || scratch > (pool ? scratch_max : 0)) {
         ctx->jit_rejected[variant] = true;
         ctx->jit_log = std::string("per-scene ") + (pool ? "pool" : "direct") + " kernel not used: " +
                        std::to_string(blocks) + " workgroups/CU (generic " + std::to_string(static_blocks) + "), " +
@@ -700,25 +707,25 @@ int jit_function(rt_context* ctx, bool pool, bool lds, size_t dyn_lds, int stati
     if (pool_waves) *pool_waves = 0;
     if (ctx->jit_failed || ctx->jit_shapes.empty()) return RT_OK;
     const int variant = (no_skips ? 4 : 0) + (pool ? 2 : 0) + (lds ? 1 : 0);
-    if (!pool) return jit_variant(ctx, variant, pool, lds, dyn_lds, static_blocks, fn, no_skips, 0);
+    if (!pool) return jit_variant(ctx, variant, pool, lds, dyn_lds, static_blocks, fn, no_skips, 0, 0);
     // The pool kernel at 7 waves/SIMD (jit_options.hpp) and, compiled beside
     // it, at the static build's occupancy: a 7-wave build that spills more
-    // than 16 B/lane is refused and the other is taken (also while the
+    // than kPool7ScratchMax is refused and the other is taken (also while the
     // 7-wave one still compiles).  Both land in the disk cache, so a later
     // process has its kernel at the first frame either way.  The 7-wave
     // build is checked against the static plan's LDS (it passes at 6
     // workgroups/CU) and the caller re-plans the pool's LDS for 7
     // (rtc_host.cpp plan_pool_for).
-    int rc = jit_variant(ctx, variant, pool, lds, dyn_lds, static_blocks, fn, no_skips, 0, true);
+    int rc = jit_variant(ctx, variant, pool, lds, dyn_lds, static_blocks, fn, no_skips, 0, 16, true);
     if (rc) return rc;
-    rc = jit_variant(ctx, variant + 8, pool, lds, dyn_lds, static_blocks, fn, no_skips, 7);
+    rc = jit_variant(ctx, variant + 8, pool, lds, dyn_lds, static_blocks, fn, no_skips, 7, kPool7ScratchMax);
     if (rc || ctx->jit_failed) return rc;
     if (*fn) {
         if (pool_waves) *pool_waves = 7;
         return RT_OK;
     }
     // (0 waves: the static build's occupancy, as planned)
-    return jit_variant(ctx, variant, pool, lds, dyn_lds, static_blocks, fn, no_skips, 0);
+    return jit_variant(ctx, variant, pool, lds, dyn_lds, static_blocks, fn, no_skips, 0, 16);
 }
 
 // Block until this context's builds in flight have finished (rt_jit_wait).
