@@ -480,19 +480,15 @@ int blocks_per_cu(rt_context* ctx, bool pool, bool lds_world, size_t lds, int* p
     return RT_OK;
 }
 
-// LDS-resident part of the ray pool: as many slots as keep the pool kernel
-// at the workgroups/CU its registers allow (6 for f32 at <= 80 VGPRs); the
-// rest of the bound spills to global memory.  RTC_DEBUG=pool_lds_rays=N overrides (A/B).
-template <typename R>
-int pool_lds_rays(rt_context* ctx, uint32_t world_lds, uint32_t cap, uint32_t* lcap) {
+// LDS-resident part of the ray pool: as many slots as keep a pool kernel at
+// the workgroups/CU its registers allow, `occ(lds, &blocks)` being its
+// occupancy at a given dynamic LDS size; the rest of the bound spills to
+// global memory.  *best: that workgroup count.
+template <typename R, typename Occ>
+int pool_lds_plan(rt_context* ctx, uint32_t world_lds, uint32_t cap, Occ&& occ, uint32_t* lcap, int* best_out) {
     constexpr uint32_t kMinRays = kBlock;
-    if (ctx->pool_lds_rays > 0) {
-        *lcap = std::min<uint32_t>(cap, std::max<uint32_t>(kMinRays, ctx->pool_lds_rays & ~7u));
-        return RT_OK;
-    }
-    const bool lw = world_lds != 0;
     int best = 0, rc;
-    if ((rc = blocks_per_cu<R>(ctx, true, lw, world_lds + pool_lds_bytes<R>(kMinRays), &best))) return rc;
+    if ((rc = occ(world_lds + pool_lds_bytes<R>(kMinRays), &best))) return rc;
     if (best < 1) best = 1;
     const size_t rec = 7 * sizeof(R) + sizeof(PoolMeta);
     const size_t budget = (size_t)kLdsPerCu / (size_t)best;
@@ -504,12 +500,26 @@ int pool_lds_rays(rt_context* ctx, uint32_t world_lds, uint32_t cap, uint32_t* l
     n = std::min<uint32_t>(cap, std::max<uint32_t>(kMinRays, n & ~7u));
     for (;;) {  // granule rounding: step down until `best` workgroups fit
         int got = 0;
-        if ((rc = blocks_per_cu<R>(ctx, true, lw, world_lds + pool_lds_bytes<R>(n), &got))) return rc;
+        if ((rc = occ(world_lds + pool_lds_bytes<R>(n), &got))) return rc;
         if (got >= best || n <= kMinRays) break;
         n = std::max<uint32_t>(kMinRays, n - 8);
     }
     *lcap = n;
+    if (best_out) *best_out = best;
     return RT_OK;
+}
+
+// ... for the static pool kernel (6 workgroups/CU for f32 at <= 80 VGPRs).
+// RTC_DEBUG=pool_lds_rays=N overrides (A/B).
+template <typename R>
+int pool_lds_rays(rt_context* ctx, uint32_t world_lds, uint32_t cap, uint32_t* lcap) {
+    if (ctx->pool_lds_rays > 0) {
+        *lcap = std::min<uint32_t>(cap, std::max<uint32_t>(kBlock, ctx->pool_lds_rays & ~7u));
+        return RT_OK;
+    }
+    const bool lw = world_lds != 0;
+    return pool_lds_plan<R>(ctx, world_lds, cap,
+                            [&](size_t lds, int* b) { return blocks_per_cu<R>(ctx, true, lw, lds, b); }, lcap, nullptr);
 }
 
 // LDS world of a per-scene kernel that takes the shape records from its
@@ -531,33 +541,18 @@ constexpr int32_t kJitRecordsMaxShapes = -1;
 // static kernel, and the resident grid with it.
 template <typename R>
 int plan_pool_for(rt_context* ctx, hipFunction_t fn, LaunchShape& ls) {
-    constexpr uint32_t kMinRays = kBlock;
-    auto blocks = [&](size_t lds, int* per_cu) -> int {
+    auto blocks = [&](size_t lds, int* per_cu) -> int {  // (blocks_per_cu's rule, for this function)
         int api = 0;
         RT_HIP(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&api, fn, kBlock, lds));
         const size_t per_block = (kStaticLds + lds + 511) / 512 * 512;
         *per_cu = std::min(api, (int)((size_t)kLdsPerCu / per_block));
         return RT_OK;
     };
-    int best = 0, rc;
-    if ((rc = blocks(ls.world_lds + pool_lds_bytes<R>(kMinRays), &best))) return rc;
-    if (best <= ls.per_cu) return RT_OK;  // no more workgroups than planned: keep the plan
-    const size_t rec = 7 * sizeof(R) + sizeof(PoolMeta);
-    const size_t budget = (size_t)kLdsPerCu / (size_t)best;
-    const size_t fixed = kStaticLds + ls.world_lds + pool_lds_bytes<R>(0) + 511;
-    uint32_t n = budget > fixed ? (uint32_t)((budget - fixed) / rec) : kMinRays;
-    const size_t room = ctx->lds_per_block > fixed ? ctx->lds_per_block - fixed : 0;
-    n = std::min<uint32_t>(n, (uint32_t)(room / rec));
-    n = std::min<uint32_t>(ls.cap, std::max<uint32_t>(kMinRays, n & ~7u));
-    for (;;) {
-        int got = 0;
-        if ((rc = blocks(ls.world_lds + pool_lds_bytes<R>(n), &got))) return rc;
-        if (got >= best || n <= kMinRays) break;
-        n = std::max<uint32_t>(kMinRays, n - 8);
-    }
-    int got = 0;
+    uint32_t n = 0;
+    int best = 0, got = 0, rc;
+    if ((rc = pool_lds_plan<R>(ctx, ls.world_lds, ls.cap, blocks, &n, &best))) return rc;
     if ((rc = blocks(ls.world_lds + pool_lds_bytes<R>(n), &got))) return rc;
-    if (got <= ls.per_cu) return RT_OK;
+    if (got <= ls.per_cu) return RT_OK;  // no more workgroups than planned: keep the plan
     ls.lcap = n;
     ls.lds = ls.world_lds + pool_lds_bytes<R>(n);
     ls.per_cu = got;
