@@ -1827,7 +1827,9 @@ __device__ inline const LaunchParams<R>& kernarg_params() {
 // VGPRs): 6 waves (80 VGPRs, 108 B/lane scratch) cover -11%, metal -7%,
 // reflect_refract/table/refraction -4..-6%, cylinders +4%; 7 and 8 waves
 // spill more and lose.  Without a cap a code change that crosses 128 VGPRs
-// drops to 3 waves (~60% slower, measured).
+// drops to 3 waves (~60% slower, measured).  Per-scene builds are also made
+// at 7 (rtc_jit.cpp jit_function, jit_options.hpp) and kept where they spill
+// little: reflect_refract, table and cover run at 7 since round 5.
 #ifndef RTC_POOL_WAVES
 #define RTC_POOL_WAVES 6
 #endif
