@@ -856,6 +856,14 @@ __device__ inline Hit<R> closest_hit(const DevScene<R>& sc, V3<R> o, V3<R> d) {
         }
         const V3<R> lo = xform_point(s.inv, o);
         const V3<R> ld = xform_vector(s.inv, d);
+        if (K == RT_SHAPE_PLANE && skips_on(sc)) {
+            // A plane's one entry is at t = -o_y / d_y (object space): with
+            // o_y d_y > 0 (nonzero, one sign) it lies behind the origin and
+            // cannot be the nearest t >= 0.  A wave whose every ray moves away
+            // from the plane skips its division and bookkeeping: exact (the
+            // product's sign is the signs' product; 0 and NaN never skip).
+            if (!wave_any(!(lo.y * ld.y > (R)0))) return;
+        }
         if constexpr (K == RT_SHAPE_CUBE && sizeof(R) == 4) {
             // A wave whose every origin lies strictly inside an enclosing cube:
             // each slab's entry is then negative and its exit positive, so the
