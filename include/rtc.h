@@ -169,13 +169,15 @@ typedef struct rt_camera_desc {
 #define RT_FLAG_GENERATIONS 32u /* also count rays per generation (generic
                                   * kernels; rt_read_generation_counts).
                                   * Pixels and rt_stats are unchanged.      */
-#define RT_FLAG_NO_SKIPS 64u    /* trace without the shadow-ray skips (light
-                                  * behind the surface, plane side, cube
-                                  * faces, blocked clusters) and the cube
-                                  * exit path: acceleration only, so pixels
-                                  * and rt_stats are unchanged (exactness
-                                  * tests; per-scene kernels get a build of
-                                  * their own)                              */
+#define RT_FLAG_NO_SKIPS 64u    /* trace without the skips: the shadow ray's
+                                  * (light behind the surface, plane side,
+                                  * cube faces, blocked clusters), the cube
+                                  * exit path, planes behind every ray of a
+                                  * wave and the containers walk's hit-point
+                                  * cull: acceleration only, so pixels and
+                                  * rt_stats are unchanged (exactness tests;
+                                  * per-scene kernels get a build of their
+                                  * own)                                    */
 
 typedef struct rt_render_options {
     uint32_t max_depth;    /* `remaining` of the primary ray; 6 = reference */
