@@ -181,6 +181,7 @@ struct rt_context {
     ncclComm_t comm = nullptr;
     int n_ranks = 1, rank = 0;
     std::vector<rt_context*> peers;  // rank 0 of a one-process group: the other devices' members
+    int32_t* d_status = nullptr;     // agree_status's word, allocated with the member so a rank can always join
     void* d_strip = nullptr;         // this member's shard strip
     size_t strip_bytes = 0;
     void* d_gathered = nullptr;      // rank 0: every strip, shard-major

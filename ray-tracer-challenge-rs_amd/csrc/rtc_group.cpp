@@ -111,6 +111,7 @@ int init_member(rt_context* m, ncclComm_t comm, int n_ranks, int rank) {
     RT_HIP(hipEventCreate(&m->ev_render0));
     RT_HIP(hipEventCreate(&m->ev_render1));
     RT_HIP(hipEventCreate(&m->ev_gather1));
+    RT_HIP(hipMalloc(reinterpret_cast<void**>(&m->d_status), sizeof(int32_t)));
     return RT_OK;
 }
 
@@ -286,35 +287,28 @@ int check_group_options(rt_context* ctx, const rt_render_options* o) {
 // RT_ERR_COMM when another rank failed, RT_OK when none did (a member's own
 // failure is returned by its caller).
 int agree_status(const std::vector<rt_context*>& ms, int local) {
-    std::vector<int32_t*> d(ms.size(), nullptr);
-    auto release = [&]() {
-        for (size_t i = 0; i < ms.size(); ++i) {
-            (void)hipSetDevice(ms[i]->device);
-            (void)hipFree(d[i]);
-        }
-    };
+    // The status words were allocated with the members (init_member), so a
+    // rank always takes part in the all-reduce: a member whose word cannot be
+    // written still joins (its stale word is overwritten by the max) and
+    // reports its own error afterwards, instead of leaving the other ranks
+    // blocked in the collective.
     const int32_t mine = local ? -local : 0;
     std::vector<int32_t> got(ms.size(), 0);
     int rc = RT_OK;
-    for (size_t i = 0; i < ms.size() && !rc; ++i) {
-        if (hipSetDevice(ms[i]->device) != hipSuccess || hipMalloc(reinterpret_cast<void**>(&d[i]), sizeof(int32_t)) != hipSuccess ||
-            hipMemcpy(d[i], &mine, sizeof mine, hipMemcpyHostToDevice) != hipSuccess)
-            rc = set_error(RT_ERR_HIP, "status exchange: device buffer");
-    }
-    if (rc) {  // (cannot take part: the other ranks' collective would wait; report it)
-        release();
-        return rc;
+    for (size_t i = 0; i < ms.size(); ++i) {
+        if (hipSetDevice(ms[i]->device) != hipSuccess ||
+            hipMemcpyAsync(ms[i]->d_status, &mine, sizeof mine, hipMemcpyHostToDevice, ms[i]->stream) != hipSuccess)
+            if (!rc) rc = set_error(RT_ERR_HIP, "status exchange: writing the status word");
     }
     ncclResult_t r = ncclGroupStart();
     for (size_t i = 0; i < ms.size() && r == ncclSuccess; ++i)
-        r = ncclAllReduce(d[i], d[i], 1, ncclInt32, ncclMax, ms[i]->comm, ms[i]->stream);
+        r = ncclAllReduce(ms[i]->d_status, ms[i]->d_status, 1, ncclInt32, ncclMax, ms[i]->comm, ms[i]->stream);
     if (r == ncclSuccess) r = ncclGroupEnd();
     for (size_t i = 0; i < ms.size() && r == ncclSuccess; ++i) {
         if (hipSetDevice(ms[i]->device) != hipSuccess || hipStreamSynchronize(ms[i]->stream) != hipSuccess ||
-            hipMemcpy(&got[i], d[i], sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
-            rc = set_error(RT_ERR_HIP, "status exchange: read back");
+            hipMemcpy(&got[i], ms[i]->d_status, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+            if (!rc) rc = set_error(RT_ERR_HIP, "status exchange: read back");
     }
-    release();
     if (r != ncclSuccess) return set_error(RT_ERR_COMM, std::string("status exchange: ") + ncclGetErrorString(r));
     if (rc) return rc;
     for (int32_t g : got)

@@ -385,19 +385,10 @@ uint32_t tile_rows_for(uint32_t height, uint32_t shards, uint32_t shard) {
 // LIFO bound of a workgroup's ray pool (rays).  Block-lockstep generations
 // pop at most `batch` rays from the top and push at most two children per
 // ray, one level deeper, so the pool never holds more than
-// kBlock + depth x batch.  The free-running variant (-DRTC_POOL_FREE): its
-// four waves each take up to `batch` (64) rays whenever idle and primaries
-// enter lanes only once the LIFO is empty; a simulation of that schedule
-// over random interleavings peaks at 2048 rays for depth 6 and 3648 for
-// depth 10, and 8 x batch x (depth + 1) leaves room above both.  Either way
-// a child past the bound is dropped and flagged (RT_ERR_POOL), never written
-// out of bounds.
+// kBlock + depth x batch.  A child past the bound would be dropped and
+// flagged (RT_ERR_POOL), never written out of bounds.
 uint32_t pool_capacity(uint32_t depth, uint32_t batch) {
-#ifdef RTC_POOL_FREE
-    return 8 * batch * (depth + 1);
-#else
     return (uint32_t)kBlock + depth * batch;
-#endif
 }
 
 // Dynamic LDS of the pool (after the world tables): the item slots'
@@ -953,21 +944,6 @@ int copy_to_host(rt_context* ctx, void* out, size_t bytes) {
     return RT_OK;
 }
 
-// The kernels' error word (LaunchParams::error_flag bits, rtc_internal.hpp).
-std::string device_error_text(int32_t err) {
-    std::string m;
-    auto add = [&](int32_t bit, const char* what) {
-        if (err & bit) m += (m.empty() ? "" : "; ") + std::string(what);
-    };
-    add(kErrPoolOverflow, "device ray pool overflow");
-    add(kErrBoundsSlot, "bounds check: pool slot outside the LIFO bound");
-    add(kErrBoundsSpill, "bounds check: spill region outside the spill buffer");
-    add(kErrBoundsTile, "bounds check: work item tile outside the launch");
-    add(kErrBoundsOut, "bounds check: output index outside the canvas");
-    add(kErrPeerTimeout, "peer canvas: a shard's flag (or the owner's release) did not arrive within the timeout");
-    return m.empty() ? "device error " + std::to_string(err) : m;
-}
-
 int check_pool_error(rt_context* ctx) {
     int32_t err = 0;
     RT_HIP(hipMemcpyAsync(&err, ctx->d_error, sizeof(err), hipMemcpyDeviceToHost, ctx->stream));
@@ -1109,6 +1085,7 @@ void destroy_device_context(rt_context* ctx) {
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     (void)hipFree(ctx->d_strip);
     (void)hipFree(ctx->d_gathered);
+    (void)hipFree(ctx->d_status);
     if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
     for (hipEvent_t e : {ctx->ev_render0, ctx->ev_render1, ctx->ev_gather1})
         if (e) (void)hipEventDestroy(e);
@@ -1202,11 +1179,21 @@ void scene_brightness(const rt_shape_desc* shapes, uint32_t ns, const rt_materia
             col[m] = std::max(col[m], std::isnan(v) ? std::numeric_limits<double>::infinity() : v);
         }
     }
+    // Children's weight: a reflective and transparent material mixes them as
+    // r·R + t·(1 − R) (world.rs:59-63), at most max(r, t) while Schlick's R
+    // stays in [0, 1] -- true when every refractive index is positive (r0 of
+    // computed_hit.rs:62 in [0, 1), cos in [0, 1]; TIR gives R = 1); the
+    // margin covers cos a rounding past 1 on an unrenormalised refracted
+    // direction (world.rs:150).  Otherwise the children add: |r| + |t|.
+    bool ri_positive = true;
+    for (uint32_t i = 0; i < nm; ++i) ri_positive = ri_positive && mats[i].refractive_index > 0.0;
     double per_light = 0.0, w = 0.0;
     for (uint32_t i = 0; i < nm; ++i) {
         const rt_material_desc& m = mats[i];
         per_light = std::max(per_light, col[i] * (std::fabs(m.ambient) + std::fabs(m.diffuse)) + std::fabs(m.specular));
-        w = std::max(w, std::fabs(m.reflectiveness) + std::fabs(m.transparency));
+        const bool mixed = ri_positive && m.reflectiveness > 0.0 && m.transparency > 0.0;
+        w = std::max(w, mixed ? std::max(m.reflectiveness, m.transparency) * (1.0 + 1e-6)
+                              : std::fabs(m.reflectiveness) + std::fabs(m.transparency));
     }
     double hit = 0.0;
     for (uint32_t l = 0; l < nl; ++l) {

@@ -53,19 +53,10 @@ RTC_HD inline void shard_of_image_row(uint32_t y, uint32_t shards, uint32_t* sha
 
 constexpr int kBlock = 256;        // threads per workgroup = 4 waves of 64
 constexpr int kWaves = kBlock / 64;  // waves per workgroup
-// The pool kernel's shape (rtc_kernels.hip trace_pool): the default build
-// runs block-lockstep generations of up to kBlock rays over one tile's pixel
-// accumulators; the free-running variant (-DRTC_POOL_FREE) lets each wave
-// take up to 64 rays at a time and holds kTileSlots items (each with its own
-// accumulators; a ray's pool meta carries its item's slot).
-#ifdef RTC_POOL_FREE
-constexpr int kTileSlots = 2;
-static_assert(kTileSlots == 2, "the pool meta carries one slot bit (pixel | slot << 8 | remaining << 9)");
-constexpr uint32_t kPoolBatch = 64;  // rays a wave takes at once
-#else
+// The pool kernel's shape (rtc_kernels.hip trace_pool): block-lockstep
+// generations of up to kBlock rays over one tile's pixel accumulators.
 constexpr int kTileSlots = 1;
 constexpr uint32_t kPoolBatch = kBlock;  // rays a generation pops
-#endif
 constexpr int kTilePixels = RT_TILE_W * RT_TILE_H;  // one tile per workgroup pass
 static_assert(kTilePixels == kBlock, "one pixel per thread per tile");
 constexpr int kNumKinds = 6;
@@ -136,11 +127,35 @@ RTC_HD inline uint64_t spill_word(uint32_t block, uint32_t spill_cap, uint32_t s
 // skips a bad access and raises one of these bits of LaunchParams::error_flag
 // (the host reports them as RT_ERR_POOL with the bit's name).
 constexpr int32_t kErrPoolOverflow = 1;  // a child beyond the LIFO bound (no debug build needed)
+constexpr int32_t kErrPoolSpin = 2;      // a pool lock's spin bound ran out (scripts/patches/pool_free_and_diag.patch only)
 constexpr int32_t kErrBoundsSlot = 4;    // pool slot outside [0, cap)
 constexpr int32_t kErrBoundsSpill = 8;   // spill record outside the launch's spill buffer
 constexpr int32_t kErrBoundsTile = 16;   // work item's tile >= n_tiles
 constexpr int32_t kErrBoundsOut = 32;    // output element outside the canvas or strip
 constexpr int32_t kErrPeerTimeout = 64;  // rt_canvas_wait: a shard's flag did not arrive in time
+constexpr int32_t kErrBitsAll[] = {kErrPoolOverflow, kErrPoolSpin, kErrBoundsSlot, kErrBoundsSpill,
+                                   kErrBoundsTile, kErrBoundsOut, kErrPeerTimeout};
+#ifndef __HIPCC_RTC__
+// The kernels' error word as rt_last_error text (RT_ERR_POOL), one distinct
+// phrase per bit (tests/index_math.cpp checks that every kErr* bit has one).
+inline std::string device_error_text(int32_t err) {
+    std::string m;
+    auto add = [&](int32_t bit, const char* what) {
+        if (err & bit) m += (m.empty() ? "" : "; ") + std::string(what);
+    };
+    add(kErrPoolOverflow, "device ray pool overflow: a child beyond the LIFO bound");
+    add(kErrPoolSpin, "device ray pool: a lock's spin bound ran out (a starved wave, not an overflow)");
+    add(kErrBoundsSlot, "bounds check: pool slot outside the LIFO bound");
+    add(kErrBoundsSpill, "bounds check: spill region outside the spill buffer");
+    add(kErrBoundsTile, "bounds check: work item tile outside the launch");
+    add(kErrBoundsOut, "bounds check: output index outside the canvas");
+    add(kErrPeerTimeout, "peer canvas: a shard's flag (or the owner's release) did not arrive within the timeout");
+    const int32_t unknown = err & ~(kErrPoolOverflow | kErrPoolSpin | kErrBoundsSlot | kErrBoundsSpill |
+                                    kErrBoundsTile | kErrBoundsOut | kErrPeerTimeout);
+    if (unknown) m += (m.empty() ? "" : "; ") + std::string("device error bits ") + std::to_string(unknown);
+    return m;
+}
+#endif
 
 // Peer canvas (rt_canvas_create): the W x H image and, after it at this
 // alignment, one u64 completion flag per shard.
@@ -196,8 +211,9 @@ template <typename R>
 using PoolAcc = long long;
 #endif
 constexpr uint32_t kAccLog2Min = 8, kAccLog2Max = 28;
-// A pool entry's meta word (pixel | slot << 8 | remaining << 9: 14 bits) as stored in
-// the LDS part of the pool; spilled entries keep 32 bits in their record.
+// A pool entry's meta word (pixel | remaining << 8: 13 bits; the pixel is the
+// lane of the workgroup's tile, 0..255) as stored in the LDS part of the
+// pool; spilled entries keep 32 bits in their record.
 #ifndef RTC_POOL_META32  // (A/B builds: -DRTC_POOL_META32 keeps 32-bit entries)
 using PoolMeta = uint16_t;
 #else

@@ -642,8 +642,13 @@ int jit_variant(rt_context* ctx, int variant, bool pool, bool lds, size_t dyn_ld
         if (b->from_disk) ++ctx->jit_cache_hits;
         ctx->jit_owner[variant] = false;
     }
+    // A failed build of the optional 7-wave variant (variant >= 8) refuses
+    // that variant only: jit_function falls back to the static-occupancy
+    // build compiled beside it.  A failed base build keeps the generic kernel
+    // for this world.
+    const bool optional = variant >= 8;
     if (state == 2) {
-        ctx->jit_failed = true;  // keep the generic kernel for this world
+        (optional ? ctx->jit_rejected[variant] : ctx->jit_failed) = true;
         ctx->jit_log = b->log;
         return RT_OK;
     }
@@ -667,7 +672,7 @@ int jit_variant(rt_context* ctx, int variant, bool pool, bool lds, size_t dyn_ld
         }
         if (e != hipSuccess) {
             (void)hipGetLastError();
-            ctx->jit_failed = true;
+            (optional ? ctx->jit_rejected[variant] : ctx->jit_failed) = true;
             ctx->jit_log = std::string("per-scene kernel not loaded (") + ctx->arch + "): " + hipGetErrorString(e);
             return RT_OK;
         }

@@ -917,9 +917,6 @@ struct Blocker {
 // lpos: the light the ray runs to (o + dist d).
 template <typename R>
 __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist, V3<R> lpos) {
-#ifdef RTC_ABLATE_SHADOW  // diagnostic builds only (scripts/build_variant.sh -DRTC_ABLATE_...): time without shadow rays
-    return false;
-#endif
     Blocker<R> b;
     const R dd = dot(d, d), rdd = recip(dd);
     const V3<R> rd = recip3(d);
@@ -1000,11 +997,6 @@ __device__ inline bool any_hit(const DevScene<R>& sc, V3<R> o, V3<R> d, R dist, 
 template <typename R, bool kDup>
 __device__ inline void refractive_indices(const DevScene<R>& sc, V3<R> o, V3<R> d, const Hit<R>& h, int hit_mat,
                                           R& n1, R& n2) {
-#ifdef RTC_ABLATE_WALK  // diagnostic builds only (scripts/build_variant.sh -DRTC_ABLATE_...): time without the walk
-    n1 = (R)1;
-    n2 = sc.lmats[hit_mat].refractive_index;
-    return;
-#endif
     struct Key {
         R t;
         int w, e;
@@ -1907,17 +1899,19 @@ __device__ inline void set_wave_prio(uint32_t p) {
     else __builtin_amdgcn_s_setprio(3);
 }
 
-// Ray pool: a LIFO of pending rays per WAVE.  Dynamic LDS after the world
-// tables holds, for the workgroup's kWaves waves:
-//   [acc: kWaves x kWaveSlots x 3 x 64 PoolAcc<R>]
-//   [wave 0: ox oy oz dx dy dz w : lds_cap x R, meta : lds_cap x u16][wave 1: ...]...
-// (meta = pixel | slot << 6 | remaining << 8 needs 13 bits; 16-bit entries
-// give the pool 1/16 more slots in the same LDS); a wave's slots [lds_cap,
-// cap) live in its region of P.spill, one 8-word record per entry (AoS: a
-// lane's entry is two dwordx4 stores / loads in f32, where the SoA layout
-// took eight dword instructions per entry).  The LIFO bound cap = batch x
-// (depth + 1) (rtc_host.cpp pool_capacity) makes overflow impossible; the
-// LDS part is sized for occupancy (plan_launch), deep excursions spill.
+// Ray pool: one LIFO of pending rays per WORKGROUP, run in block-lockstep
+// generations (trace_pool).  Dynamic LDS after the world tables holds
+//   [acc: kTileSlots (1) x 3 x kBlock PoolAcc<R>: the tile's pixel sums]
+//   [ox oy oz dx dy dz w : lds_cap x R][meta : lds_cap x PoolMeta]
+// with meta = pixel | remaining << 8 (pixel = the lane of the 64x4 tile,
+// 0..255; 13 bits, so 16-bit entries give the pool 1/16 more slots in the
+// same LDS; rtc_internal.hpp PoolMeta).  Slots [lds_cap, cap) live in the
+// workgroup's region of P.spill, one 8-word record per entry (AoS: a lane's
+// entry is two dwordx4 stores / loads in f32, where the SoA layout took
+// eight dword instructions per entry; the record keeps meta in 32 bits).
+// The LIFO bound cap = kBlock + depth x batch (rtc_host.cpp pool_capacity)
+// makes overflow impossible; the LDS part is sized for occupancy
+// (plan_launch), deep excursions spill.
 template <typename R>
 struct Pool {
     PoolAcc<R>* acc;
@@ -2082,11 +2076,10 @@ __device__ inline bool item_pixel(const LaunchParams<R>& P, uint32_t t, uint32_t
     return tile_pixel(P, t, tid, x, y, out_idx);
 }
 
-#ifndef RTC_POOL_FREE
-// trace_pool (default build): the recursion as a per-workgroup LIFO ray
-// pool run in block-lockstep generations (rounds 1-4).  The
-// free-running variant (-DRTC_POOL_FREE, below) drops the per-generation
-// barriers; it is kept for the A/B of DESIGN.md §3.2.
+// trace_pool: the recursion as a per-workgroup LIFO ray pool run in
+// block-lockstep generations.  The round-5 free-running
+// variant that dropped the per-generation barriers (slower, §3.2) is kept
+// out of the product source as scripts/patches/pool_free_and_diag.patch.
 template <typename R, bool kLds, bool kDup>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 4 ? RTC_POOL_WAVES : 1))) void trace_pool(
     LaunchParams<R> P, RTC_WORLD_PARAMS(R)) {
@@ -2184,14 +2177,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
             };
             if (active) hit = shade_ray<R, true, kDup>(sc, ro, rd, meta >> 8, sh, push);
             count_events(k, false, hit, sh, sc.n_lights);
-#ifdef RTC_ITER_DIAG  // (diagnostic builds: lane slots and active lanes in place of counters 5 and 6)
-            k.c[5] += 64 - wave_count(hit & sh.patterned) * (uint32_t)sc.n_lights;
-            k.c[6] += wave_count(active) - wave_count(hit & sh.refr_eval);
-#endif
-#ifdef RTC_WALK_DIAG  // (diagnostic builds: waves that ran the walk x 64 and walking lanes in counters 5 and 6)
-            k.c[5] += (wave_any(hit & sh.schlick) ? 64u : 0u) - wave_count(hit & sh.patterned) * (uint32_t)sc.n_lights;
-            k.c[6] += wave_count(hit & sh.schlick) - wave_count(hit & sh.refr_eval);
-#endif
 #ifndef RTC_JIT  // (per-scene builds never take RT_FLAG_GENERATIONS launches)
             if (P.gen_counts) count_generations(P.gen_counts, active, hit, meta >> 8);
 #endif
@@ -2241,417 +2226,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     }
 }
 
-#else  // RTC_POOL_FREE
-// The pool kernel's shared state of a workgroup (static LDS).  The ray LIFO
-// is shared by the workgroup's four waves, which run free: a wave takes rays
-// whenever its lanes are idle and pushes children as it makes them, so the
-// LIFO's top and the item cursor change under a lock (a wave's pops must not
-// meet another's reserved, unwritten pushes).  Items in flight: kTileSlots,
-// each with pixel accumulators; `out` counts an item's unfinished rays
-// (unissued primaries included) and is changed by atomics outside the lock.
-struct PoolShared {
-    uint32_t lock[2];        // ticket lock: next ticket, now serving
-    int top;                 // LIFO size
-    int cur;                 // slot whose primaries are being issued, -1 = none
-    uint32_t issued;         // primaries of slot `cur` taken so far
-    uint32_t next_item;      // the workgroup's next item (fetched ahead), kItemFetching or kItemDone
-    uint32_t tile[kTileSlots];
-    uint32_t range[kTileSlots];  // base | count << 9 | split << 18 | prio << 22
-    uint32_t start_lo[kTileSlots], start_hi[kTileSlots];
-    int32_t out[kTileSlots];
-    int32_t open[kTileSlots];
-};
-constexpr uint32_t kItemFetching = 0xFFFFFFFEu;  // a wave is dequeuing it
-// Polls of an idle wave with no progress before it gives up (~1 s; a frame's
-// longest item takes well under 1 ms): a lost ray cannot occur, but no wave
-// may wait on one forever.
-constexpr uint32_t kPoolSpinLimit = 1u << 21;
-constexpr uint32_t kItemDone = kNoItem;         // the launch's queue is drained
-__device__ inline uint32_t slot_range(uint32_t base, uint32_t count, uint32_t split, uint32_t prio) {
-    return base | count << 9 | split << 18 | prio << 22;
-}
-
-// LDS ticket lock of the workgroup (FIFO-fair: a wave waiting to push a
-// child must not starve behind idle waves polling for work), taken by the
-// first active lane of the calling lanes (callable under divergence);
-// acquire/release order the LIFO and cursor accesses around it.
-__device__ inline void pool_lock(uint32_t* l) {
-    const unsigned long long m = __builtin_amdgcn_ballot_w64(true);
-    if ((int)(threadIdx.x & 63) == __ffsll((long long)m) - 1) {
-        const uint32_t t = atomicAdd(&l[0], 1u);
-        while (__hip_atomic_load(&l[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != t)
-            __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-__device__ inline void pool_unlock(uint32_t* l) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    const unsigned long long m = __builtin_amdgcn_ballot_w64(true);
-    if ((int)(threadIdx.x & 63) == __ffsll((long long)m) - 1) atomicAdd(&l[1], 1u);
-}
-
-// Dequeue the next work item for the workgroup from the per-XCD queues (one
-// lane of a wave; the caller's `probe` remembers drained queues, as
-// next_tile).  kItemDone once every queue is.
-template <typename R>
-__device__ inline uint32_t fetch_item(const LaunchParams<R>& P, uint32_t& probe, uint32_t n_items) {
-    for (; probe < (uint32_t)kTileQueues; ++probe) {
-        const uint32_t q = (blockIdx.x + probe) % kTileQueues;
-        const unsigned long long j = atomicAdd(&P.tile_counter[q * kQueueStride], 1ull);
-        const unsigned long long i = q + (unsigned long long)kTileQueues * j;
-        if (i < n_items) return P.tile_order ? P.tile_order[i] : (uint32_t)i;
-    }
-    return kItemDone;
-}
-
-// Slot s is complete (its `out` reached 0: no ray of it is left anywhere):
-// its pixels out, its accumulators zeroed, its cost recorded, the slot free.
-// All lanes of the wave call it.
-template <typename R>
-__device__ inline void flush_slot(const LaunchParams<R>& P, PoolAcc<R>* acc, PoolShared& S, int s, uint32_t lane,
-                                  bool diag) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // every wave's accumulator adds before the reads
-    const uint32_t tile = S.tile[s], range = S.range[s];
-    const uint32_t base = range & 0x1FFu, count = (range >> 9) & 0x1FFu, split = (range >> 18) & 0xFu;
-    const double acc_inv = sizeof(PoolAcc<R>) == 4 ? __builtin_ldexp(1.0, -(int)P.acc_log2) : kAccInvScale;
-    PoolAcc<R>* a = acc + s * 3 * kBlock;
-    for (uint32_t i = lane; i < count; i += 64) {
-        const uint32_t t_tid = base + i;
-        uint64_t out_idx = 0;
-        bool ok = item_pixel(P, tile, t_tid, out_idx);
-#ifdef RTC_BOUNDS_CHECK
-        ok &= in_bounds(!ok || out_idx < (P.rays ? P.n_rays
-                                                : (uint64_t)(P.image_rows ? P.height : P.tile_rows * RT_TILE_H) *
-                                                      P.width),
-                        P.error_flag, kErrBoundsOut);
-#endif
-        const V3<R> c = {(R)((double)a[t_tid] * acc_inv), (R)((double)a[kBlock + t_tid] * acc_inv),
-                         (R)((double)a[2 * kBlock + t_tid] * acc_inv)};
-        if (ok) store_pixel(P, out_idx, c);
-        a[t_tid] = 0;
-        a[kBlock + t_tid] = 0;
-        a[2 * kBlock + t_tid] = 0;
-    }
-    if (lane == 0 && (P.tile_cost || (diag && P.item_log))) {
-        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-        const unsigned long long start = S.start_lo[s] | (unsigned long long)S.start_hi[s] << 32;
-        const uint32_t c = (uint32_t)min(now - start, (unsigned long long)(0x0FFFFFFFu >> split));
-        // (a split tile: its slowest part times the parts, order_tiles zeroed it)
-#ifndef RTC_POOL_DIAG
-        if (P.tile_cost) {
-            if (split) atomicMax(&P.tile_cost[tile], c << split);
-            else P.tile_cost[tile] = c;
-        }
-#endif
-        if (diag && P.item_log) {  // diagnostics (RT_FLAG_STAMPS): the item's span
-            const unsigned long long q = atomicAdd(&P.item_log[0], 1ull);
-            const uint32_t code = P.tile_order ? encode_item(tile, base >> (8 - split), split, range >> 22) : tile;
-            P.item_log[1 + 3 * q] = code | (unsigned long long)blockIdx.x << 32;
-            P.item_log[2 + 3 * q] = start;
-            P.item_log[3 + 3 * q] = now;
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // accumulators zeroed before the slot reopens
-    if (lane == 0) __hip_atomic_store(&S.open[s], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// trace_pool: the recursion as a workgroup ray pool whose four waves run
-// free, with no barrier between the first (world staging) and the last
-// (counter flush).  Each iteration a wave
-//   * takes rays for its idle lanes from the top of the workgroup's LIFO
-//     and, once it is empty, primary rays of the open work item, opening
-//     the next item (fetched ahead) into a free slot when that one is fully
-//     issued (kTileSlots items in flight, so lanes a finishing item leaves
-//     idle take the next item's primaries);
-//   * traces one ray per lane (closest hit, shading with any-hit shadow
-//     rays) and pushes the children where they are made (ballot + mbcnt,
-//     one reservation per wave and push site);
-//   * adds weight x surface into the item's fixed-point pixel sums (LDS
-//     atomics: order-independent, so frames are bit-identical to any other
-//     schedule) and counts the item's rays down; the wave that finishes an
-//     item's last ray writes its pixels.
-// The LIFO's top holds the children most recently made, of one item and of
-// neighbouring pixels, so a wave's lanes stay as coherent as the batches of
-// rounds 1-4, which ran the pool in block-lockstep generations (pop,
-// barrier, shade, barrier): there every generation waited for its slowest
-// wave (11-21 % of a wave's time at the barrier).
-template <typename R, bool kLds, bool kDup>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 4 ? RTC_POOL_WAVES : 1))) void trace_pool(
-    LaunchParams<R> P0, RTC_WORLD_PARAMS(R)) {
-    extern __shared__ __align__(16) unsigned char smem_all[];
-    __shared__ PoolShared S;
-    (void)scene_view<R, kLds>(P0, shapes, materials, patterns, lights, smem_all, false);
-    // (per-scene pool builds keep the diagnostics: same-box A/B without them
-    // reflect_refract, refraction, metal within 1 %)
-    constexpr bool kDiag = true;
-    const uint32_t tid = threadIdx.x, lane = tid % 64;
-    if (kDiag && P0.stamps && tid == 0) P0.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-    const uint32_t n_items = P0.item_count ? *P0.item_count : P0.n_tiles;
-    uint32_t probe = 0;  // (lane 0 of a fetching wave)
-    {
-        PoolAcc<R>* acc = reinterpret_cast<PoolAcc<R>*>(smem_all + (kLds ? P0.world_lds : 0));
-        for (int i = tid; i < kTileSlots * 3 * kBlock; i += kBlock) acc[i] = 0;
-        if (kLds) {  // the world tables (scene_view's staging, here without its barrier)
-            const uint4* s4 = reinterpret_cast<const uint4*>(kJitRecords && sizeof(R) == 4 ? (const void*)materials
-                                                                                          : (const void*)shapes);
-            uint4* d4 = reinterpret_cast<uint4*>(smem_all);
-            for (uint32_t i = tid; i < P0.world_lds / 16; i += kBlock) d4[i] = s4[i];
-        }
-        if (tid == 0) {
-            S.lock[0] = S.lock[1] = 0;
-            S.top = 0;
-            S.cur = -1;
-            S.issued = 0;
-            for (int s = 0; s < kTileSlots; ++s) S.open[s] = S.out[s] = 0;
-            // Two sets of queue heads alternate between dynamic launches: this
-            // launch zeroes the set the next one uses (its last user, the
-            // previous launch, has completed: stream order).
-            if (blockIdx.x == 0)
-                for (int q = 0; q < kTileQueues; ++q) P0.next_tile_counter[q * kQueueStride] = 0ull;
-            S.next_item = fetch_item(P0, probe, n_items);
-        }
-        __syncthreads();
-    }
-
-    Counts k = {};
-    bool fetcher = false;  // (wave-uniform) this wave took the prefetched item and fetches the next
-    uint32_t prio = 0;
-    uint32_t spins = 0;
-    for (;;) {
-        // The launch's parameters from the kernarg segment at each use (held
-        // in SGPRs across the loop, they spilled: kernarg_params).
-        const LaunchParams<R>& P = kernarg_params<R>();
-        const DevScene<R> sc = scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem_all);
-        unsigned char* smem = smem_all + (kLds ? P.world_lds : 0);
-        const int cap = (int)P.pool_capacity;
-        Pool<R> pl;
-        pl.acc = reinterpret_cast<PoolAcc<R>*>(smem);
-        pl.lds = reinterpret_cast<R*>(smem + kTileSlots * 3 * kBlock * sizeof(PoolAcc<R>));
-        pl.lds_cap = (int)P.pool_lds_capacity;
-        pl.spill = reinterpret_cast<R*>(P.spill) + spill_word(blockIdx.x, cap - pl.lds_cap, pl.lds_cap, pl.lds_cap);
-        pl.spill_cap = cap - pl.lds_cap;
-#ifdef RTC_BOUNDS_CHECK
-        pl.err = P.error_flag;
-        if (!in_bounds(cap == pl.lds_cap || blockIdx.x < P.spill_blocks, P.error_flag, kErrBoundsSpill))
-            pl.spill_cap = 0;
-#endif
-        if (fetcher) {  // the item after the one this wave opened
-            uint32_t it = 0;
-            if (lane == 0) {
-                it = fetch_item(P, probe, n_items);
-                __hip_atomic_store(&S.next_item, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            fetcher = false;
-        }
-
-        // ---- take rays: the LIFO's top, then primaries (under the lock)
-        const int batch = (int)P.pop_batch;
-        bool has = false, primary = false;
-        V3<R> ro = {(R)0, (R)0, (R)0}, rd = {(R)0, (R)0, (R)0};
-        R rw = (R)0;
-        uint32_t meta = 0, p_tile = 0, p_tid = 0;
-        if (spins) {
-            // an idle wave looks before it locks: nothing on the LIFO, no
-            // primaries left, no item to open
-            bool work = __hip_atomic_load(&S.top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > 0 ||
-                        __hip_atomic_load(&S.cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= 0;
-            const uint32_t nx = __hip_atomic_load(&S.next_item, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            bool open_all = true;
-            for (int s = 0; s < kTileSlots; ++s)
-                open_all &= __hip_atomic_load(&S.open[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
-            work |= nx != kItemDone && nx != kItemFetching && !open_all;
-            if (!__builtin_amdgcn_readfirstlane((int)work)) {
-                if (nx == kItemDone && !(__hip_atomic_load(&S.open[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) |
-                                         __hip_atomic_load(&S.open[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
-                    break;
-                if (++spins > kPoolSpinLimit) {  // (a lost ray: cannot happen; bounded anyway)
-                    atomicOr(P.error_flag, kErrPoolOverflow);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(8);
-                continue;
-            }
-        }
-        pool_lock(S.lock);
-        {
-            const int top = __builtin_amdgcn_readfirstlane(S.top);
-            const int take = top < batch ? top : batch;
-            if ((int)lane < take) {
-                pool_get(pl, top - take + (int)lane, ro, rd, rw, meta);
-                has = true;
-            }
-            if (lane == 0) S.top = top - take;
-            int first = take;
-            while (first < batch) {  // (wave-uniform)
-                int cur = __builtin_amdgcn_readfirstlane(S.cur);
-                if (cur < 0) {  // open the prefetched item in a free slot
-                    int free_slot = -1;
-                    for (int s = kTileSlots - 1; s >= 0; --s)
-                        if (!__builtin_amdgcn_readfirstlane(S.open[s])) free_slot = s;
-                    const uint32_t item =
-                        (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(&S.next_item, __ATOMIC_RELAXED,
-                                                                                        __HIP_MEMORY_SCOPE_WORKGROUP));
-                    if (free_slot < 0 || item == kItemDone || item == kItemFetching) break;
-                    // packed fields only in items handed out through a tile
-                    // order (raster items are plain tile indices, any number of them)
-                    const WorkItem wi = decode_item(item, P.tile_order != nullptr);
-#ifdef RTC_BOUNDS_CHECK
-                    if (!in_bounds(wi.tile < P.n_tiles, P.error_flag, kErrBoundsTile)) {
-                        if (lane == 0) S.next_item = kItemFetching;
-                        fetcher = true;
-                        break;
-                    }
-#endif
-                    const uint32_t count = (uint32_t)kBlock >> wi.split_log2;
-                    if (lane == 0) {
-                        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-                        S.tile[free_slot] = wi.tile;
-                        S.range[free_slot] = slot_range(wi.part * count, count, wi.split_log2, wi.prio);
-                        S.start_lo[free_slot] = (uint32_t)now;
-                        S.start_hi[free_slot] = (uint32_t)(now >> 32);
-                        S.out[free_slot] = (int32_t)count;
-                        S.open[free_slot] = 1;
-                        S.cur = free_slot;
-                        S.issued = 0;
-                        S.next_item = kItemFetching;
-                    }
-                    fetcher = true;
-                    cur = free_slot;
-                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                }
-                const uint32_t range = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.range[cur]);
-                const uint32_t count = (range >> 9) & 0x1FFu;
-                const uint32_t issued = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.issued);
-                const int left = (int)(count - issued);
-                const int n = batch - first < left ? batch - first : left;
-                if ((int)lane >= first && (int)lane < first + n) {
-                    p_tile = S.tile[cur];
-                    p_tid = (range & 0x1FFu) + issued + (lane - (uint32_t)first);
-                    meta = p_tid | (uint32_t)cur << 8 | (P.max_depth << 9);
-                    has = primary = true;
-                }
-                if (lane == 0) {
-                    S.issued = issued + (uint32_t)n;
-                    if (issued + (uint32_t)n == count) S.cur = -1;
-                }
-                first += n;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            }
-        }
-        pool_unlock(S.lock);
-        if (!wave_any(has)) {
-            // nothing to trace: done when no item can open or is open, else
-            // another wave's rays may still make children
-            bool busy = __hip_atomic_load(&S.next_item, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != kItemDone;
-            for (int s = 0; s < kTileSlots; ++s)
-                busy |= __hip_atomic_load(&S.open[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
-            if (!__builtin_amdgcn_readfirstlane((int)busy) && !fetcher) break;
-#ifdef RTC_POOL_DIAG
-            if (++spins > kPoolSpinLimit) {
-                if (P.tile_cost && lane == 0) {
-                    atomicAdd(&P.tile_cost[3], 1u);
-                    P.tile_cost[8] = (uint32_t)S.out[0];
-                    P.tile_cost[9] = (uint32_t)S.out[1];
-                    P.tile_cost[10] = (uint32_t)S.open[0];
-                    P.tile_cost[11] = (uint32_t)S.open[1];
-                    P.tile_cost[12] = S.next_item;
-                    P.tile_cost[13] = (uint32_t)S.top;
-                    P.tile_cost[14] = (uint32_t)S.cur;
-                    P.tile_cost[15] = S.issued;
-                    P.tile_cost[16] = blockIdx.x;
-                    P.tile_cost[17] = threadIdx.x;
-                    P.tile_cost[18] = S.lock[0] - S.lock[1];
-                }
-#else
-            if (++spins > kPoolSpinLimit) {  // (a lost ray: cannot happen; bounded anyway)
-#endif
-                atomicOr(P.error_flag, kErrPoolOverflow);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(4);
-            continue;
-        }
-        bool valid = has;
-        if (primary) {
-            uint64_t out_idx;
-            load_primary(P, p_tile, p_tid, valid, ro, rd, out_idx);
-            rw = (R)1;
-        }
-        k.c[0] += wave_count(primary & valid);
-        // the costliest item among the wave's rays sets its priority (order_tiles)
-        {
-            uint32_t p = 0;
-            for (int s = 0; s < kTileSlots; ++s)
-                if (wave_any(has && ((meta >> 8) & 1u) == (uint32_t)s))
-                    p = max(p, (uint32_t)__builtin_amdgcn_readfirstlane((int)S.range[s]) >> 22);
-            if (p != prio) set_wave_prio(p);
-            prio = p;
-        }
-
-        // ---- trace one ray per lane; children pushed where they are made
-        auto push = [&](V3<R> co, V3<R> cd, R cw) {
-            const unsigned long long m = __builtin_amdgcn_ballot_w64(true);
-            const int prefix = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-            pool_lock(S.lock);
-            const int base = __builtin_amdgcn_readfirstlane(S.top);
-            const int at = base + prefix;
-            const bool stored = at < cap;
-            if (stored) pool_put(pl, at, co, cd, rw * cw, (meta & 0x1FFu) | ((((meta >> 9) & 0x1Fu) - 1u) << 9));
-            else atomicOr(P.error_flag, kErrPoolOverflow);  // (beyond the bound: dropped, flagged)
-            // the item's count rises before another wave can take the child
-            const int n1 = __popcll(__builtin_amdgcn_ballot_w64(stored && ((meta >> 8) & 1u)));
-            const int n0 = __popcll(__builtin_amdgcn_ballot_w64(stored && !((meta >> 8) & 1u)));
-            if (prefix == 0) {
-#ifdef RTC_POOL_DIAG
-                if (P.tile_cost) {
-                    atomicMax(&P.tile_cost[0], (uint32_t)(base + __popcll(m)));
-                    if (base + __popcll(m) > cap) atomicAdd(&P.tile_cost[1], 1u);
-                    atomicMax(&P.tile_cost[2], (meta >> 9) & 0x1Fu);
-                }
-#endif
-                S.top = min(base + __popcll(m), cap);
-                if (n1) atomicAdd(&S.out[1], n1);
-                if (n0) atomicAdd(&S.out[0], n0);
-            }
-            pool_unlock(S.lock);
-        };
-        Shaded<R> sh;
-        bool hit = false;
-        if (valid) hit = shade_ray<R, true, kDup>(sc, ro, rd, (meta >> 9) & 0x1Fu, sh, push);
-        count_events(k, false, hit, sh, sc.n_lights);
-#ifndef RTC_JIT  // (per-scene builds never take RT_FLAG_GENERATIONS launches)
-        if (P.gen_counts) count_generations(P.gen_counts, valid, hit, (meta >> 9) & 0x1Fu);
-#endif
-        const uint32_t slot = (meta >> 8) & 1u;
-        if (hit) {
-            PoolAcc<R>* a = pl.acc + slot * 3 * kBlock;
-            const uint32_t pix = meta & 0xFFu;
-            const float acc_scale = __builtin_ldexpf(1.0f, (int)P.acc_log2);
-            acc_add(a, pix, sh.surface.x * rw, acc_scale);
-            acc_add(a + kBlock, pix, sh.surface.y * rw, acc_scale);
-            acc_add(a + 2 * kBlock, pix, sh.surface.z * rw, acc_scale);
-        }
-        // ---- the wave's rays end: count their items down; the wave that
-        // ends an item's last ray writes its pixels
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // accumulator adds before the count
-        for (int s = 0; s < kTileSlots; ++s) {
-            const int n = (int)wave_count(has && slot == (uint32_t)s);
-            if (!n) continue;
-            int old = 0;
-            if (lane == 0) old = atomicSub(&S.out[s], n);
-            if (__builtin_amdgcn_readfirstlane(old) == n) flush_slot(P, pl.acc, S, s, lane, kDiag);
-        }
-        spins = 0;
-    }
-    if (prio) __builtin_amdgcn_s_setprio(0);
-    if (!(P0.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P0.counters);
-    if (kDiag && P0.stamps) {
-        __syncthreads();
-        if (threadIdx.x == 0) P0.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-    }
-}
-
-#endif  // RTC_POOL_FREE
 
 #ifndef RTC_PRECISION
 #define RTC_PRECISION 0

@@ -158,7 +158,8 @@ def share_camera(camera, rank: int, src: int = 0):
 def collective_call(fn, rank: int, device="cpu"):
     """Run one rank's part of a collective librtc step (fn() on this rank)
     and agree on its outcome before anyone goes on: every rank contributes
-    its status (0, or the RenderError code it raised) to one all-reduce, and
+    its status (0, the RenderError code it raised, or 1 for any other
+    exception) to one all-reduce, and
     if any rank failed, every rank raises (the failing ones their own error,
     the others RT_ERR_COMM naming the first failing rank).  So a rank that
     fails its upload cannot leave the others waiting in the next collective
@@ -171,7 +172,7 @@ def collective_call(fn, rank: int, device="cpu"):
     err, result = None, None
     try:
         result = fn()
-    except RenderError as e:
+    except Exception as e:  # noqa: BLE001  (any failure must still reach the all-reduce)
         err = e
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         if err is not None:
@@ -180,7 +181,10 @@ def collective_call(fn, rank: int, device="cpu"):
     world = dist.get_world_size()
     # per rank: 0 = ok, else -code (codes are negative): one MAX reduce of a world-long vector
     st = torch.zeros(world, dtype=torch.int64, device=device)
-    st[rank] = 0 if err is None else max(1, -int(err.code))
+    # a RenderError contributes its code, anything else (a ValueError or
+    # OSError of the Python upload path) a generic nonzero status
+    code = int(getattr(err, "code", 0) or 0) if isinstance(err, RenderError) else -1
+    st[rank] = 0 if err is None else max(1, -code)
     dist.all_reduce(st, op=dist.ReduceOp.MAX)
     if err is not None:
         raise err

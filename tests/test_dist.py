@@ -165,7 +165,7 @@ def test_camera_reaches_every_rank_bit_exact(tmp_path, rtc):
         assert open(f"{out}.{r}", "rb").read() == ref
 
 
-def _fail_worker(rank, world, port, out_path):
+def _fail_worker(rank, world, port, out_path, kind="render"):
     """Rank 1's upload fails (a malformed table: RT_ERR_INVALID from the
     library's validation, stood in for here since a group context needs GPUs);
     the step's status agreement must make every rank raise, then a later
@@ -180,14 +180,18 @@ def _fail_worker(rank, world, port, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         def upload():
-            if rank == 1:
+            if rank == 1 and kind == "render":
                 raise rtc_amd.RenderError(rtc_amd.RT_ERR_INVALID, "shape 3: material index out of range")
+            if rank == 1:
+                raise OSError("scene file vanished")  # not a RenderError
             return "uploaded"
         try:
             rdist.collective_call(upload, rank)
             code = 0
         except rtc_amd.RenderError as e:
             code = e.code
+        except OSError:
+            code = 99
         t = torch.tensor([1.0])
         dist.all_reduce(t)  # the group is still usable
         with open(f"{out_path}.{rank}", "w") as f:
@@ -196,17 +200,19 @@ def _fail_worker(rank, world, port, out_path):
         dist.destroy_process_group()
 
 
-def test_a_rank_failing_its_upload_fails_every_rank(tmp_path):
+@pytest.mark.parametrize("kind", ["render", "os"])
+def test_a_rank_failing_its_upload_fails_every_rank(tmp_path, kind):
     import time
 
     import torch.multiprocessing as mp
     world = 2
     out = str(tmp_path / "status")
     t0 = time.monotonic()
-    ctx = mp.spawn(_fail_worker, args=(world, _free_port(), out), nprocs=world, join=False)
+    ctx = mp.spawn(_fail_worker, args=(world, _free_port(), out, kind), nprocs=world, join=False)
     while not ctx.join(timeout=5):
         assert time.monotonic() - t0 < 120, "a rank is still waiting after another failed its upload"
     codes = [open(f"{out}.{r}").read().split() for r in range(world)]
-    assert int(codes[1][0]) == -1            # RT_ERR_INVALID on the failing rank
+    # the failing rank re-raises its own exception: RT_ERR_INVALID, or the OSError
+    assert int(codes[1][0]) == (-1 if kind == "render" else 99)
     assert int(codes[0][0]) == -8            # RT_ERR_COMM on the others
     assert all(float(c[1]) == 2.0 for c in codes)

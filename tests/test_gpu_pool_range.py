@@ -58,3 +58,26 @@ def test_test_pattern_on_a_plane_is_refused_by_the_pool(gpu_ctx, rtc, precision)
     # depth 0 runs the direct kernel, which sums nothing: no bound is needed
     img, _ = gpu_ctx.render(cam, 0, precision=precision)
     assert np.isfinite(img).all()
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_glass_world_at_the_deepest_supported_depth(gpu_ctx, rtc, oracle, precision):
+    """the bound once summed reflectiveness + transparency
+    (1.8 for reflect_refract's glass), so (1.8^17 - 1)/0.8 put the f64 bound
+    past 2^14 and refused depth 16.  A reflective and transparent material
+    mixes its children by Schlick's R and 1 - R (world.rs:59-63), so their
+    weight is at most max(r, t) = 0.9 and the frame renders."""
+    from conftest import scene_fixture
+    scene = scene_fixture("reflect_refract")
+    cam = rtc.camera_resize(scene.camera, 96, 64)
+    depth = rtc.RT_MAX_SUPPORTED_DEPTH
+    gpu_ctx.upload(scene)
+    img, st = gpu_ctx.render(cam, depth, precision=precision)
+    ref, ref_st = oracle.render(scene, cam, depth, threads=8)
+    for k in ("primary", "shadow", "reflect", "refract"):
+        assert st[k] == ref_st[k] or precision == "f32", (k, st[k], ref_st[k])
+    if precision == "f64":
+        assert np.abs(img - ref).max() < 1e-9
+    else:
+        d = np.abs(oracle.quantize(img).astype(int) - oracle.quantize(ref.astype(np.float64)).astype(int)).max(axis=2)
+        assert (d <= 2).mean() >= 0.97

@@ -26,7 +26,13 @@ def test_index_math_cpp(tmp_path):
     subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-o", str(exe), os.path.join(HERE, "index_math.cpp")],
                    check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True)
-    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stdout + out.stderr
+    lines = out.stdout.split()
+    assert out.returncode == 0 and lines[-1] == "ok", out.stdout + out.stderr
+    # kErrBitsAll lists every kErr* constant of the header
+    import re
+    hdr = open(os.path.join(HERE, "..", "ray-tracer-challenge-rs_amd", "csrc", "rtc_internal.hpp")).read()
+    declared = re.findall(r"constexpr int32_t (kErr\w+) = ", hdr)
+    assert f"errbits {len(declared)}" in out.stdout, (declared, out.stdout)
 
 
 def _pool_peak(depth, seeds, rng, children):
