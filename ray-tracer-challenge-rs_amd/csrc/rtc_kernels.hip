@@ -68,6 +68,23 @@ struct Real;
 #ifndef RTC_F32_REL_OFFSET
 #define RTC_F32_REL_OFFSET 3e-5f
 #endif
+// Flat kinds (planes, cubes, triangles: t from one division per face, so
+// the hit point is off the surface by a few ulps of the ray's coordinates):
+// RTC_F32_FLAT_OFFSET x max(1, |p|inf, |o|inf) = 16 f32 ulps of the larger
+// of hit point and ray origin.  RTC_F32_FLAT_KINDS: bit k = shape kind k
+// takes it (0: every kind takes the quadric offset, round 5's product).
+#ifndef RTC_F32_FLAT_OFFSET
+#define RTC_F32_FLAT_OFFSET 1.9073486e-6f
+#endif
+#ifndef RTC_F32_FLAT_KINDS
+#define RTC_F32_FLAT_KINDS 38
+#endif
+// Spheres: RTC_F32_SPHERE_OFFSET x max(1, |p|inf) (cylinders and cones keep
+// RTC_F32_REL_OFFSET: cylinders.yaml stands them on the floor, and smaller
+// offsets meet the coplanar cap on the wrong side).
+#ifndef RTC_F32_SPHERE_OFFSET
+#define RTC_F32_SPHERE_OFFSET RTC_F32_REL_OFFSET
+#endif
 template <>
 struct Real<float> {
     static constexpr float kEps = 8e-8f;        // guards (consts.rs:2)
@@ -103,10 +120,20 @@ struct Real<float> {
     // 1e-4 put refraction.yaml 95.5 % within 2/255 of the oracle, a fixed
     // 1e-5 98.6 % but self-shadowed shadow_puppets' backdrop at |p| ~ 20
     // (97.2 %); the hardware rcp/sqrt/exp/log approximations change nothing.
-    __device__ static inline float surface_offset(float px, float py, float pz) {
-        const float m = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(px), __builtin_fabsf(py)),
-                                        __builtin_fmaxf(__builtin_fabsf(pz), 1.0f));
-        return RTC_F32_REL_OFFSET * m;
+    //
+    // Round 6: planes and cubes take their own, smaller offset (above,
+    // RTC_F32_FLAT_OFFSET): table.yaml floats its glass cube 1e-5 above the
+    // table top (table.yaml:131-136), a tenth of 3e-5 x 3.45, so rays
+    // reflected off the table under the cube started inside the glass and
+    // table lost 3 % of its refractions.
+    // cls: 0 sphere, 1 flat kind, 2 cylinder or cone (offset_class)
+    __device__ static inline float surface_offset(float px, float py, float pz, float ox, float oy, float oz,
+                                                  int cls) {
+        const float mp = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(px), __builtin_fabsf(py)),
+                                         __builtin_fmaxf(__builtin_fabsf(pz), 1.0f));
+        const float mo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(ox), __builtin_fabsf(oy)),
+                                         __builtin_fmaxf(__builtin_fabsf(oz), mp));
+        return cls == 1 ? RTC_F32_FLAT_OFFSET * mo : (cls == 0 ? RTC_F32_SPHERE_OFFSET : RTC_F32_REL_OFFSET) * mp;
     }
 };
 
@@ -127,7 +154,9 @@ struct Real<double> {
     __device__ static inline double fabs(double a) { return __builtin_fabs(a); }
     __device__ static inline double fmax(double a, double b) { return __builtin_fmax(a, b); }
     __device__ static inline double fmin(double a, double b) { return __builtin_fmin(a, b); }
-    __device__ static inline double surface_offset(double, double, double) { return kOffset; }
+    __device__ static inline double surface_offset(double, double, double, double, double, double, int) {
+        return kOffset;
+    }
 };
 
 template <typename R>
@@ -1386,8 +1415,35 @@ __device__ inline void count_events(Counts& k, bool primary, bool hit, const Sha
 template <typename R>
 struct Prepared {
     V3<R> p, n, eye, over, base;
+    R off;    // the over/under-point offset (computed_hit.rs:33-34; f32: per kind)
     int mat;  // the hit's material index
 };
+
+// The hit's offset class for Real<float>::surface_offset: 1 for the flat
+// kinds of RTC_F32_FLAT_KINDS, 0 for spheres, 2 otherwise.  Per-scene builds
+// with records know the kind from the slot's range (constants).
+__device__ inline int offset_class_of_kind(int kind) {
+    return ((RTC_F32_FLAT_KINDS >> (kind & 31)) & 1) ? 1 : (kind == RT_SHAPE_SPHERE ? 0 : 2);
+}
+
+template <typename R>
+__device__ inline int offset_class(const Hit<R>& h) {
+#ifdef RTC_JIT
+    if constexpr (sizeof(R) == 4) {
+        int c = 2;
+#pragma unroll
+        for (int k = 0; k < kNumKinds; ++k)
+            if (h.slot >= jit::kBegin[k] && h.slot < jit::kBegin[k + 1]) c = offset_class_of_kind(k);
+        return c;
+    }
+#endif
+    return offset_class_of_kind(h.kind);
+}
+
+template <typename R>
+__device__ inline R hit_offset(const Hit<R>& h, V3<R> p, V3<R> o) {
+    return Real<R>::surface_offset(p.x, p.y, p.z, o.x, o.y, o.z, offset_class(h));
+}
 
 #ifdef RTC_JIT
 // The per-scene direct kernel (no pool, few live values): prepare_hit with
@@ -1402,7 +1458,8 @@ __device__ inline void prepare_hit_const(const DevScene<float>& sc, V3<float> o,
     q.eye = vneg(d);
     if (dot(q.n, q.eye) < 0.0f) q.n = vneg(q.n);
     q.mat = -1;  // (the direct kernel walks no refractive indices)
-    q.over = along(q.p, q.n, Real<float>::surface_offset(q.p.x, q.p.y, q.p.z));
+    q.off = hit_offset(h, q.p, o);
+    q.over = along(q.p, q.n, q.off);
     q.base = {m.color[0], m.color[1], m.color[2]};
     patterned = m.pattern >= 0;
     if (jit::kPatterns && patterned) {
@@ -1428,7 +1485,8 @@ __device__ inline const MaterialRec<R>& prepare_hit(const DevScene<R>& sc, V3<R>
         if (dot(q.n, q.eye) < (R)0) q.n = vneg(q.n);
         q.mat = mat;
         const MaterialRec<R>& m = sc.lmats[mat];
-        q.over = along(q.p, q.n, Real<R>::surface_offset(q.p.x, q.p.y, q.p.z));
+        q.off = hit_offset(h, q.p, o);
+        q.over = along(q.p, q.n, q.off);
         q.base = {m.color[0], m.color[1], m.color[2]};
         patterned = m.pattern >= 0;
         if (jit::kPatterns && patterned) {
@@ -1446,7 +1504,8 @@ __device__ inline const MaterialRec<R>& prepare_hit(const DevScene<R>& sc, V3<R>
     if (dot(q.n, q.eye) < (R)0) q.n = vneg(q.n);
     q.mat = s.material;
     const MaterialRec<R>& m = sc.lmats[s.material];
-    q.over = along(q.p, q.n, Real<R>::surface_offset(q.p.x, q.p.y, q.p.z));
+    q.off = hit_offset(h, q.p, o);
+        q.over = along(q.p, q.n, q.off);
     q.base = {m.color[0], m.color[1], m.color[2]};
     patterned = m.pattern >= 0;
 #ifdef RTC_JIT
@@ -1526,6 +1585,7 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
     const MaterialRec<R>& m = prepare_hit(sc, o, d, h, q, out.patterned);
 #endif
     const V3<R> p = q.p, n = q.n, eye = q.eye, over = q.over, base = q.base;
+    const R off = q.off;
     V3<R> surface = {(R)0, (R)0, (R)0};
     for_lights(sc, [&](const LightRec<R>& L) {
         const V3<R> lpos = {L.position[0], L.position[1], L.position[2]};
@@ -1597,7 +1657,7 @@ __device__ inline bool shade_ray(const DevScene<R>& sc, V3<R> o, V3<R> d, uint32
                 const R cos_t = T::sqrt((R)1 - sin2_t);
                 const R f = T::rfma(nr, cos_i, -cos_t);
                 out.refr_child = true;
-                push(along(p, n, -T::surface_offset(p.x, p.y, p.z)),  // under_point, computed_hit.rs:34
+                push(along(p, n, -off),  // under_point, computed_hit.rs:34
                      V3<R>{n.x * f - eye.x * nr, n.y * f - eye.y * nr, n.z * f - eye.z * nr}, m.transparency * ft);
             }
         }

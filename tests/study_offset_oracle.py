@@ -19,22 +19,34 @@ import tempfile
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 OFFSETS = ("3e-6", "3e-5")
+# (curved, flat, origin term) of the per-kind rule: the f32 product's
+# (Real<float>::surface_offset: 3e-5 on quadrics, 16 f32 ulps of
+# max(1, |p|, |o|) = 1.9e-6 x that on planes and cubes)
+PER_KIND = (("3e-5", "1.9e-6", True), ("3e-5", "4.8e-7", True))
 SRC = "    c.over_point = add(c.point, scale(c.normal, EPSILON));\n    c.under_point = sub(c.point, scale(c.normal, EPSILON));"
+# per-kind: planes, cubes and triangles (t from one division) take OFFFLAT x
+# max(1, |p|inf, |o|inf); spheres and quadrics OFFREL x max(1, |p|inf).  A
+# single offset for every kind is OFFFLAT = OFFREL with the origin term off.
 REL = ("    { const double m = std::fmax(1.0, std::fmax(std::fabs(c.point.x), std::fmax(std::fabs(c.point.y), "
-       "std::fabs(c.point.z))));\n      c.over_point = add(c.point, scale(c.normal, OFFREL * m));\n"
-       "      c.under_point = sub(c.point, scale(c.normal, OFFREL * m)); }")
+       "std::fabs(c.point.z))));\n"
+       "      const double mo = std::fmax(m, std::fmax(std::fabs(ray.origin.x), std::fmax(std::fabs(ray.origin.y), "
+       "std::fabs(ray.origin.z))));\n"
+       "      const bool flat = hit.shape->kind == S_PLANE || hit.shape->kind == S_CUBE || hit.shape->kind == S_TRIANGLE;\n"
+       "      const double off = flat ? OFFFLAT * (ORIGIN ? mo : m) : OFFREL * m;\n"
+       "      c.over_point = add(c.point, scale(c.normal, off));\n"
+       "      c.under_point = sub(c.point, scale(c.normal, off)); }")
 
 
-def build(tmp, x):
+def build(tmp, x, flat=None, origin=False):
     hdr = open(os.path.join(ROOT, "oracle", "rtc_oracle.hpp")).read()
     assert SRC in hdr, "prepare_computations changed: update this study"
-    d = os.path.join(tmp, x)
+    d = os.path.join(tmp, f"{x}_{flat}_{int(origin)}")
     os.makedirs(d)
     open(os.path.join(d, "rtc_oracle.hpp"), "w").write(hdr.replace(SRC, REL))
     capi = open(os.path.join(ROOT, "oracle", "oracle_capi.cpp")).read()
     open(os.path.join(d, "oracle_capi.cpp"), "w").write(capi)
     lib = os.path.join(d, "liboracle.so")
-    subprocess.run(["g++", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", f"-DOFFREL={x}",
+    subprocess.run(["g++", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", f"-DOFFREL={x}", f"-DOFFFLAT={flat or x}", f"-DORIGIN={int(origin)}",
                     f"-I{os.path.join(ROOT, 'include')}", f"-I{os.path.join(ROOT, 'oracle')}", "-o", lib,
                     os.path.join(d, "oracle_capi.cpp"), "-lpthread"], check=True)
     return lib
@@ -59,10 +71,13 @@ def main():
     scenes = sys.argv[1:] or ["table", "cylinders"]
     base = {r["scene"]: r for r in counts("", scenes)}
     with tempfile.TemporaryDirectory() as tmp:
-        for x in OFFSETS:
-            for r in counts(build(tmp, x), scenes):
+        runs = [(x, None, False, f"{x} x max(1,|p|inf)") for x in OFFSETS]
+        runs += [(c, f, o, f"quadrics {c} x max(1,|p|inf), flat {f} x max(1,|p|inf{',|o|inf' if o else ''})")
+                 for c, f, o in PER_KIND]
+        for x, flat, origin, label in runs:
+            for r in counts(build(tmp, x, flat, origin), scenes):
                 b = base[r["scene"]]
-                print(json.dumps({"offset": f"{x} x max(1,|p|inf)", "scene": r["scene"],
+                print(json.dumps({"offset": label, "scene": r["scene"],
                                   **{k: [r[k], round((r[k] - b[k]) / max(1, b[k]), 6)]
                                      for k in ("shadow", "reflect", "refract")}}))
 
