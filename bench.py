@@ -81,6 +81,8 @@ def parse():
                          "measured too and reported under gather_variants")
     ap.add_argument("--ab", action="store_true",
                     help="A/B runs: skip the one-shot child, the host-frame latency and the per-generation frame")
+    ap.add_argument("--stream", choices=["side", "null"], default="side",
+                    help="the launch stream: a stream of the bench's own (default) or HIP's null stream")
     ap.add_argument("--one-shot-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -409,7 +411,10 @@ def measure(args, tiled, world, rank, local):
     t_first = time.perf_counter()
     scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{args.scene}.json")) if rank == 0 else None
     phase = {"scene_load_ms": (time.perf_counter() - t_first) * 1e3}
-    stream = torch.cuda.current_stream()
+    # the frames run on a stream of their own (HIP's null stream orders every
+    # launch against the device's other blocking streams; --stream null keeps
+    # it for the A/B)
+    stream = torch.cuda.Stream() if args.stream == "side" else torch.cuda.current_stream()
     sptr = stream.cuda_stream
     rdtype = torch.uint8 if args.out == "u8" else (torch.float32 if args.precision == "f32" else torch.float64)
     if tiled:
@@ -607,6 +612,7 @@ def measure(args, tiled, world, rank, local):
                        "max_depth": args.depth, "out": args.out,
                        "parallelism": f"{'tiles' if tiled else 'frames'}x{world}",
                        "rays_per_frame": int(total_rays // args.steps) if tiled else int(rays // args.steps),
+                       "stream": args.stream,
                        "mode": "tiled" if tiled else "frames"},
             # the path is FP32-VALU bound: no MFMA, the compute roof is the vector ALU's
             "roofline": {"bound": "valu", "pipe": f"valu-{args.precision}", "achieved": achieved, "peak": peak,
