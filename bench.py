@@ -171,6 +171,8 @@ def device_state(local: int) -> dict:
     build: current gfx and memory clocks (MHz), socket power and its cap (W),
     hotspot temperature (C), and the throttle status when the metrics table
     has one.  {"error": ...} when amdsmi is unavailable (never fails the line)."""
+    if os.environ.get("BENCH_NO_SMI"):
+        return {"skipped": "BENCH_NO_SMI"}
     try:
         import amdsmi
         if "handle" not in _SMI:

@@ -1884,14 +1884,6 @@ __device__ inline const LaunchParams<R>& kernarg_params() {
 #ifndef RTC_DIRECT_WAVES
 #define RTC_DIRECT_WAVES 8
 #endif
-// Per-scene direct builds: read the launch parameters through the kernel's
-// own argument, so the compiler may keep the loop-invariant ones (camera,
-// canvas, tile counts) in SGPRs across the tile loop instead of re-loading
-// them per tile (kernarg_params; the direct build with its records as
-// constants has SGPRs to spare: 40 of them in use).
-#ifndef RTC_DIRECT_HOIST
-#define RTC_DIRECT_HOIST 0
-#endif
 // Waves per SIMD of the f32 pool kernel (VGPRs <= 512 / waves; its LDS pool
 // is sized to match, rtc_host.cpp pool_lds_rays).  Occupancy beats spills
 // here: same-box A/B (scripts/ab_builds.sh), kernel time vs 4 waves (111
@@ -1924,9 +1916,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     // grid.  Primary-only tiles cost the same, so no queue is needed, and the
     // tile index is an SGPR by construction (loop control stays scalar).
     for (uint32_t t = blockIdx.x;; t += gridDim.x) {
-#if !(defined(RTC_JIT) && RTC_DIRECT_HOIST)
         const LaunchParams<R>& P = kernarg_params<R>();
-#endif
         const DevScene<R> sc = scene_view<R, kLds>(P, shapes, materials, patterns, lights, smem);
         if (t >= P.n_tiles) break;
         bool valid;

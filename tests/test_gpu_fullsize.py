@@ -14,7 +14,7 @@ agree bit for bit, and the per-scene frame is the one held to the tolerance.
 
 Tolerances are the suite's: f64 every pixel within 1e-9 and all eight
 counters identical; f32 per scene the observed agreement plus a stated margin
-(tests/f32_tolerance.py, from profiles/r05_parity.json).  The oracle
+(tests/f32_tolerance.py, from profiles/r06_parity.json).  The oracle
 renders each frame once per session on ORACLE_THREADS host threads (a few
 seconds per 4K frame on the GPU box's 16).  The multi-GPU split of
 configs[3]/[4] (cyclic RT_TILE_H-row blocks) is checked on one
