@@ -409,6 +409,12 @@ def measure(args, tiled, world, rank, local):
     import rtc_amd
     from rtc_amd import dist as rdist
     from rtc_amd import scene_io
+    # The device state before anything of this workload runs: an amdsmi query
+    # next to the timed region slowed its frames by 20 % (round 6, same box,
+    # three_sphere 1080p: 15.7 -> 18.8 us per frame with a sample right
+    # before the region), so the samples are taken here, ahead
+    # of the >= 200 ms warm-up, and after the region's clock has stopped.
+    state_before = device_state(local)
     # Only rank 0 holds the world, as the reference's single caller does
     t_first = time.perf_counter()
     scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{args.scene}.json")) if rank == 0 else None
@@ -496,13 +502,9 @@ def measure(args, tiled, world, rank, local):
     # previous one's tail — see scripts/host_overhead.py): average = bracket / K.
     # Tiled: the bracket is rank 0's stream (its shard, the gather, the de-interleave).
     timed = timed_launches(step, stream, args.steps)
-    state_before = device_state(local)  # (amdsmi reads sysfs, no HIP call; ms, so before the re-warm)
-    # The GPU must not sit idle between the warm-up and the timed region: the
-    # events, the device-state sample and the barrier above cost milliseconds,
-    # and a K = 20 region that starts on an idled GPU ran its frames 10-20 %
-    # slower (round 6: 21.9 us per step against 16.1 us after a warm burst on
-    # the same build; scripts/graph_probe.py).  So ~2 ms of untimed frames
-    # keep it busy across the barrier; the region itself is unchanged.
+    # The GPU should not sit idle between the warm-up and the timed region
+    # (the events and the barrier above cost milliseconds): ~2 ms of untimed
+    # frames keep it busy across them; the region itself is unchanged.
     burst = max(2, int(2.0 / max(warm_ms_per_frame, 1e-3)) + 1)
     for _ in range(burst):
         step()
@@ -634,7 +636,9 @@ def measure(args, tiled, world, rank, local):
         line.update(extra)
         # clocks, power and temperature just before and just after the timed
         # region (tell a slower box from a box-sensitive build)
-        line["device_state"] = {"before": state_before, "after": state_after}
+        line["device_state"] = {"before": state_before, "after": state_after,
+                                "note": "before: ahead of the warm-up (an amdsmi query right before the "
+                                        "region slows it); after: once the region's clock has stopped"}
         line["rays_by_kind"] = by_kind
         line["first_frame_ms"] = first_frame_ms
         line["first_frame_breakdown"] = phase
