@@ -2155,10 +2155,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     if (kDiag && P.stamps && threadIdx.x == 0) P.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     unsigned char* smem = smem_all + (kLds ? P.world_lds : 0);
     __shared__ int s_top[2];
-    __shared__ unsigned int s_item[kPoolSlotsMax];  // the open item of each slot (kNoItem: free)
-    __shared__ int s_live[kPoolSlotsMax];           // its rays in the pool
-    __shared__ unsigned int s_next;                 // the next item from the queues (thread 0 fetches it)
-    __shared__ unsigned long long s_start[kPoolSlotsMax];  // s_memrealtime when the item opened
+    __shared__ int s_live[kPoolSlotsMax];           // rays of each open item in the pool
+    __shared__ unsigned int s_next[2];              // the next item from the queues (thread 0 fetches it)
+    __shared__ unsigned long long s_start[kPoolSlotsMax];  // thread 0: s_memrealtime when the item opened
     const uint32_t cap = P.pool_capacity;
     const uint32_t lcap = P.pool_lds_capacity, gcap = cap - lcap;
     Pool<R> pl;
@@ -2188,15 +2187,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     uint32_t fetched = 0;  // thread 0: items taken from the queues so far
     if (tid == 0) {
         s_top[0] = 0;
-        for (int s = 0; s < kPoolSlotsMax; ++s) {
-            s_item[s] = kNoItem;
-            s_live[s] = 0;
-        }
-        s_next = next_tile(P, fetched++, probe, n_items);
+        for (int s = 0; s < kPoolSlotsMax; ++s) s_live[s] = 0;
+        s_next[0] = next_tile(P, fetched++, probe, n_items);
     }
     for (int i = (int)tid; i < nslots * 3 * kBlock; i += kBlock) pl.acc[i] = 0;
     __syncthreads();
-    uint32_t prio_now = 0;
+    // The open items live in registers, the same in every thread (every
+    // thread opens and closes the same items in the same generations):
+    // item[s] of slot s, kNoItem when free.  Shared words are read only
+    // where no wave can be changing them: s_next alternates between two
+    // words (thread 0 fetches into the one not being read), the pool's top
+    // and the live counts are read after the barrier that completes their
+    // atomics and before the barrier after which they change.
+    uint32_t item[kPoolSlotsMax];
+    for (int s = 0; s < kPoolSlotsMax; ++s) item[s] = kNoItem;
+    uint32_t opens = 0, prio_now = 0;
     const uint32_t lane = tid & 63u;
     // Generations of the workgroup's LIFO.  An item (a tile, or a part of a
     // split tile) opens into a free slot of accumulators by pushing its
@@ -2210,20 +2215,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     for (uint32_t gen = 0;; ++gen) {
         const int cur = gen & 1;
         {
-            const uint32_t next = __builtin_amdgcn_readfirstlane(s_next);
-            const int size0 = __builtin_amdgcn_readfirstlane(s_top[cur]);
+            const uint32_t next = __builtin_amdgcn_readfirstlane(s_next[opens & 1]);
             int free_slot = -1, n_open = 0;
             for (int s = 0; s < nslots; ++s) {
-                const bool open = __builtin_amdgcn_readfirstlane(s_item[s]) != kNoItem;
-                n_open += open ? 1 : 0;
-                if (!open && free_slot < 0) free_slot = s;
+                n_open += item[s] != kNoItem ? 1 : 0;
+                if (item[s] == kNoItem && free_slot < 0) free_slot = s;
             }
             if (next == kNoItem && n_open == 0) break;  // drained: every item written
-            if (next != kNoItem && free_slot >= 0 && (n_open == 0 || size0 < (int)P.refill_below)) {
+            bool open = false;
+            if (next != kNoItem && free_slot >= 0) {
+                if (n_open == 0) {
+                    open = true;  // (the pool is empty: every item closed)
+                } else if (P.refill_below) {
+                    // the pool's size, final since the generation's last barrier;
+                    // the seeds below change it only after every wave has read it
+                    open = __builtin_amdgcn_readfirstlane(s_top[cur]) < (int)P.refill_below;
+                    if (open) __syncthreads();
+                }
+            }
+            if (open) {
                 // packed fields only in items handed out through a tile order (raster
                 // items are plain tile indices, any number of them)
                 const WorkItem wi = decode_item(next, P.tile_order != nullptr);
-                bool valid;
+                bool valid = false;
                 V3<R> o, d;
                 uint64_t out_idx;
 #ifdef RTC_BOUNDS_CHECK
@@ -2242,17 +2256,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
                              tid | ((uint32_t)free_slot << kMetaSlotShift) | (P.max_depth << kMetaRemShift));
                 if (lane == 0 && seeds) atomicAdd(&s_live[free_slot], (int)seeds);
                 if (tid == 0) {
-                    s_item[free_slot] = next;
                     s_start[free_slot] = __builtin_amdgcn_s_memrealtime();
-                    s_next = next_tile(P, fetched++, probe, n_items);
+                    s_next[(opens + 1) & 1] = next_tile(P, fetched++, probe, n_items);
                 }
+                item[free_slot] = next;
+                ++opens;
                 // the costliest items set the launch's tail: their waves win issue
                 // arbitration against the other workgroups' on the same SIMDs
                 if (wi.prio > prio_now) {
                     prio_now = wi.prio;
                     set_wave_prio(prio_now);
                 }
-                __syncthreads();  // seeds pushed, the slot taken
+                __syncthreads();  // seeds pushed and counted, the next item fetched
             }
         }
         const int size = s_top[cur];  // (0 when the items open have no pixel left in the canvas)
@@ -2276,9 +2291,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
         // one LDS atomic per wave) at the point the child is made
         auto push = [&](V3<R> co, V3<R> cd, R cw) {
             const int slot = wave_reserve(true, &s_top[cur ^ 1]);
-            if (slot < (int)cap) pool_put(pl, slot, co, cd, rw * cw, child_meta);
-            else atomicOr(P.error_flag, kErrPoolOverflow);
-            ++pushed;
+            if (slot < (int)cap) {
+                pool_put(pl, slot, co, cd, rw * cw, child_meta);
+                ++pushed;
+            } else {
+                atomicOr(P.error_flag, kErrPoolOverflow);
+            }
         };
         if (active) hit = shade_ray<R, true, kDup>(sc, ro, rd, rem, sh, push);
         count_events(k, false, hit, sh, sc.n_lights);
@@ -2291,7 +2309,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
             acc_add(acc + kBlock, pix, sh.surface.y * rw, acc_scale);
             acc_add(acc + 2 * kBlock, pix, sh.surface.z * rw, acc_scale);
         }
-        // each slot's live rays: -1 per ray traced, +1 per child pushed (one
+        // each slot's live rays: -1 per ray traced, +1 per child stored (one
         // LDS atomic per wave and slot)
         for (int s = 0; s < nslots; ++s) {
             const bool mine = active && rslot == (uint32_t)s;
@@ -2300,7 +2318,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
             if (lane == 0 && delta) atomicAdd(&s_live[s], delta);
         }
         __syncthreads();  // pushes and counts complete before the next pop
-        if (s_top[cur ^ 1] > (int)cap) {  // overflowed: drop the pool (error already flagged)
+        // An overflow (never, by the bound; the error is flagged) drops the
+        // pool and closes the open items with what they have.
+        if (__builtin_amdgcn_readfirstlane(s_top[cur ^ 1]) > (int)cap) {
             __syncthreads();
             if (tid == 0) {
                 s_top[cur ^ 1] = 0;
@@ -2309,10 +2329,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
             __syncthreads();
         }
         // Close the items none of whose rays is left: write their pixels.
+        bool closed = false;
         for (int s = 0; s < nslots; ++s) {
-            const uint32_t item = __builtin_amdgcn_readfirstlane(s_item[s]);
-            if (item == kNoItem || __builtin_amdgcn_readfirstlane(s_live[s]) != 0) continue;
-            const WorkItem wi = decode_item(item, P.tile_order != nullptr);
+            if (item[s] == kNoItem || __builtin_amdgcn_readfirstlane(s_live[s]) != 0) continue;
+            closed = true;
+            const WorkItem wi = decode_item(item[s], P.tile_order != nullptr);
             const uint32_t t = wi.tile;
             uint64_t out_idx = 0;
             bool valid = t < P.n_tiles && item_pixel(P, t, tid, out_idx) && item_seeds(tid, wi);
@@ -2340,24 +2361,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
             }
             if (kDiag && tid == 0 && P.item_log) {  // diagnostics (RT_FLAG_STAMPS): the item's span
                 const unsigned long long n = atomicAdd(&P.item_log[0], 1ull);
-                P.item_log[1 + 3 * n] = item | (unsigned long long)blockIdx.x << 32;
+                P.item_log[1 + 3 * n] = item[s] | (unsigned long long)blockIdx.x << 32;
                 P.item_log[2 + 3 * n] = s_start[s];
                 P.item_log[3 + 3 * n] = __builtin_amdgcn_s_memrealtime();
             }
-            __syncthreads();  // every thread read the slot before it is freed
-            if (tid == 0) s_item[s] = kNoItem;
-            __syncthreads();
+            item[s] = kNoItem;
             // wave priority: the highest of the items still open
             uint32_t p = 0;
-            for (int q = 0; q < nslots; ++q) {
-                const uint32_t iq = __builtin_amdgcn_readfirstlane(s_item[q]);
-                if (iq != kNoItem) p = max(p, decode_item(iq, P.tile_order != nullptr).prio);
-            }
+            for (int q = 0; q < nslots; ++q)
+                if (item[q] != kNoItem) p = max(p, decode_item(item[q], P.tile_order != nullptr).prio);
             if (p != prio_now) {
                 prio_now = p;
                 set_wave_prio(p);
             }
         }
+        // Every wave has read the live counts (and zeroed its accumulator
+        // entries) before an item opens into a freed slot.
+        if (closed) __syncthreads();
     }
     if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
     if (kDiag && P.stamps) {
