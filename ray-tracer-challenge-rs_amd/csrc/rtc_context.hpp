@@ -127,10 +127,6 @@ struct rt_context {
     // 0.130 / 0.096 / 0.115; reflect_refract 1080p of 4 0.127 / 0.128 /
     // 0.121, of 16 0.112 / 0.092 / 0.097; whole frames split nothing.
     uint32_t split_max = 3;
-    // Item refill in the pool kernel (rtc_kernels.hip trace_pool): a second
-    // item opens into the workgroup's LIFO while fewer than `refill` rays are
-    // left to pop (0 = one item at a time).  RTC_DEBUG=refill=N.
-    uint32_t refill = 0;
     // Items (tiles or parts) costing more than urgent_factor x the mean
     // workgroup load run at raised wave priority, graded 1/2/3 above 1x/2x/4x
     // that cost (RTC_DEBUG=urgent=F, 0 = none; one level for all measured no better).  Same-box sweep, kernel ms, none / flat 0.25 / flat 0.125 /

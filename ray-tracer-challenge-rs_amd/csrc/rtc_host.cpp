@@ -385,25 +385,18 @@ uint32_t tile_rows_for(uint32_t height, uint32_t shards, uint32_t shard) {
 // LIFO bound of a workgroup's ray pool (rays).  Block-lockstep generations
 // pop at most `batch` rays from the top and push at most two children per
 // ray, one level deeper, so the pool never holds more than
-// kBlock + depth x batch.  With item refill a second item's primaries (at
-// most kBlock) are pushed only while fewer than `batch` rays are left, which
-// adds at most kBlock (tests/test_index_math.py models both).  A child past
-// the bound would be dropped and flagged (RT_ERR_POOL), never written out of
-// bounds.
-uint32_t pool_capacity(uint32_t depth, uint32_t batch, bool refill = false) {
-    return (uint32_t)kBlock * (refill ? 2u : 1u) + depth * batch;
+// kBlock + depth x batch.  A child past the bound would be dropped and
+// flagged (RT_ERR_POOL), never written out of bounds.
+uint32_t pool_capacity(uint32_t depth, uint32_t batch) {
+    return (uint32_t)kBlock + depth * batch;
 }
-
-// Item slots of the pool kernel: 2 with item refill, else 1.
-inline uint32_t pool_slots(const rt_context* ctx) { return ctx->refill ? 2u : 1u; }
 
 // Dynamic LDS of the pool (after the world tables): the item slots'
 // accumulators, then `lcap` LIFO slots (a multiple of 8 keeps every array
 // 16-byte aligned).
 template <typename R>
-size_t pool_lds_bytes(const rt_context* ctx, uint32_t lcap) {
-    return (size_t)pool_slots(ctx) * 3 * kBlock * sizeof(PoolAcc<R>) +
-           (size_t)lcap * (7 * sizeof(R) + sizeof(PoolMeta));
+size_t pool_lds_bytes(uint32_t lcap) {
+    return (size_t)kTileSlots * 3 * kBlock * sizeof(PoolAcc<R>) + (size_t)lcap * (7 * sizeof(R) + sizeof(PoolMeta));
 }
 
 // Bound on any pixel of the pool kernel: a shaded hit adds at most
@@ -486,11 +479,11 @@ template <typename R, typename Occ>
 int pool_lds_plan(rt_context* ctx, uint32_t world_lds, uint32_t cap, Occ&& occ, uint32_t* lcap, int* best_out) {
     constexpr uint32_t kMinRays = kBlock;
     int best = 0, rc;
-    if ((rc = occ(world_lds + pool_lds_bytes<R>(ctx, kMinRays), &best))) return rc;
+    if ((rc = occ(world_lds + pool_lds_bytes<R>(kMinRays), &best))) return rc;
     if (best < 1) best = 1;
     const size_t rec = 7 * sizeof(R) + sizeof(PoolMeta);
     const size_t budget = (size_t)kLdsPerCu / (size_t)best;
-    const size_t fixed = kStaticLds + world_lds + pool_lds_bytes<R>(ctx, 0) + 511;
+    const size_t fixed = kStaticLds + world_lds + pool_lds_bytes<R>(0) + 511;
     uint32_t n = budget > fixed ? (uint32_t)((budget - fixed) / rec) : kMinRays;
     // one workgroup's LDS must also stay within the launch limit
     const size_t room = ctx->lds_per_block > fixed ? ctx->lds_per_block - fixed : 0;
@@ -498,7 +491,7 @@ int pool_lds_plan(rt_context* ctx, uint32_t world_lds, uint32_t cap, Occ&& occ, 
     n = std::min<uint32_t>(cap, std::max<uint32_t>(kMinRays, n & ~7u));
     for (;;) {  // granule rounding: step down until `best` workgroups fit
         int got = 0;
-        if ((rc = occ(world_lds + pool_lds_bytes<R>(ctx, n), &got))) return rc;
+        if ((rc = occ(world_lds + pool_lds_bytes<R>(n), &got))) return rc;
         if (got >= best || n <= kMinRays) break;
         n = std::max<uint32_t>(kMinRays, n - 8);
     }
@@ -549,10 +542,10 @@ int plan_pool_for(rt_context* ctx, hipFunction_t fn, LaunchShape& ls) {
     uint32_t n = 0;
     int best = 0, got = 0, rc;
     if ((rc = pool_lds_plan<R>(ctx, ls.world_lds, ls.cap, blocks, &n, &best))) return rc;
-    if ((rc = blocks(ls.world_lds + pool_lds_bytes<R>(ctx, n), &got))) return rc;
+    if ((rc = blocks(ls.world_lds + pool_lds_bytes<R>(n), &got))) return rc;
     if (got <= ls.per_cu) return RT_OK;  // no more workgroups than planned: keep the plan
     ls.lcap = n;
-    ls.lds = ls.world_lds + pool_lds_bytes<R>(ctx, n);
+    ls.lds = ls.world_lds + pool_lds_bytes<R>(n);
     ls.per_cu = got;
     const uint64_t resident = (uint64_t)got * (uint64_t)ctx->cu_count;
     ls.grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ls.grid_tiles, resident));
@@ -575,9 +568,9 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
     if (ls.pool) {
         // (the pool kernel takes its items from the per-XCD queues only)
         ls.batch = kPoolBatch;
-        ls.cap = pool_capacity(depth, ls.batch, ctx->refill != 0);
+        ls.cap = pool_capacity(depth, ls.batch);
         if ((rc = pool_lds_rays<R>(ctx, ls.world_lds, ls.cap, &ls.lcap))) return rc;
-        ls.lds += pool_lds_bytes<R>(ctx, ls.lcap);
+        ls.lds += pool_lds_bytes<R>(ls.lcap);
     }
     int per_cu = 0;
     if ((rc = blocks_per_cu<R>(ctx, ls.pool, ls.world_lds != 0, ls.lds, &per_cu))) return rc;
@@ -776,8 +769,6 @@ int launch(rt_context* ctx, DeviceWorld<R>& w, const rt_camera_desc* cam, const 
     P.pool_capacity = ls.cap;
     P.pool_lds_capacity = ls.lcap;
     P.pop_batch = ls.batch;
-    P.pool_slots = pool_slots(ctx);
-    P.refill_below = ctx->refill;
     if (ls.pool && (rc = check_pixel_range(ctx, depth, sizeof(R) == 4))) return rc;
     P.acc_log2 = acc_shift_f32(ctx->bright_hit, ctx->bright_w, depth);
     if (ls.cap > ls.lcap) {
@@ -1036,7 +1027,6 @@ int create_device_context(int device_ordinal, rt_context** out) {
     if (debug_knob("split_max", &v))
         ctx->split_max = (uint32_t)std::min<int>((int)kMaxSplitLog2, std::max(0, std::atoi(v.c_str())));
     if (debug_knob("urgent", &v)) ctx->urgent_factor = std::atof(v.c_str());
-    if (debug_knob("refill", &v)) ctx->refill = (uint32_t)std::min(kBlock, std::max(0, std::atoi(v.c_str())));
     // RTC_JIT: the per-scene build mode (rt_context_set_jit's values), a user setting
     if (const char* e = std::getenv("RTC_JIT"))
         ctx->jit_mode = (e[0] >= '0' && e[0] <= '3' && !e[1]) ? e[0] - '0' : RT_JIT_AUTO;

@@ -54,9 +54,8 @@ RTC_HD inline void shard_of_image_row(uint32_t y, uint32_t shards, uint32_t* sha
 constexpr int kBlock = 256;        // threads per workgroup = 4 waves of 64
 constexpr int kWaves = kBlock / 64;  // waves per workgroup
 // The pool kernel's shape (rtc_kernels.hip trace_pool): block-lockstep
-// generations of up to kBlock rays over the pixel accumulators of up to
-// kPoolSlotsMax open items (a second one only with item refill).
-constexpr int kPoolSlotsMax = 2;
+// generations of up to kBlock rays over one tile's pixel accumulators.
+constexpr int kTileSlots = 1;
 constexpr uint32_t kPoolBatch = kBlock;  // rays a generation pops
 constexpr int kTilePixels = RT_TILE_W * RT_TILE_H;  // one tile per workgroup pass
 static_assert(kTilePixels == kBlock, "one pixel per thread per tile");
@@ -212,17 +211,15 @@ template <typename R>
 using PoolAcc = long long;
 #endif
 constexpr uint32_t kAccLog2Min = 8, kAccLog2Max = 28;
-// A pool entry's meta word (pixel | slot << 8 | remaining << 9: 14 bits; the
-// pixel is the lane of its item's tile, 0..255, the slot the item's
-// accumulators) as stored in the LDS part of the pool; spilled entries keep
-// 32 bits in their record.
-constexpr uint32_t kMetaSlotShift = 8, kMetaRemShift = 9;
+// A pool entry's meta word (pixel | remaining << 8: 13 bits; the pixel is the
+// lane of the workgroup's tile, 0..255) as stored in the LDS part of the
+// pool; spilled entries keep 32 bits in their record.
 #ifndef RTC_POOL_META32  // (A/B builds: -DRTC_POOL_META32 keeps 32-bit entries)
 using PoolMeta = uint16_t;
 #else
 using PoolMeta = uint32_t;
 #endif
-static_assert(RT_MAX_SUPPORTED_DEPTH < 128, "remaining must fit the pool meta's 7 high bits");
+static_assert(RT_MAX_SUPPORTED_DEPTH < 32, "remaining must fit the pool meta's 8 high bits");
 
 // ShapeRec::flags.  Value-equal shapes (shape_identity.hpp) form one identity
 // class; its members are adjacent within their kind's run of the table, the
@@ -347,9 +344,7 @@ struct LaunchParams {
     uint32_t max_depth;      // `remaining` of the primary ray
     uint32_t pool_capacity;  // pool kernel: LIFO bound (rays) per workgroup
     uint32_t pool_lds_capacity;  // of which held in LDS; the rest in `spill`
-    uint32_t pop_batch;      // pool kernel: rays a generation pops (<= kBlock)
-    uint32_t pool_slots;     // pool kernel: items open at once (1, or 2 with refill)
-    uint32_t refill_below;   // pool kernel: open the next item while fewer rays than this are left (0 = off)
+    uint32_t pop_batch;      // pool kernel: rays a wave traces per iteration (<= 64)
     uint32_t acc_log2;       // f32 pool kernel: pixel sums in int32 multiples of 2^-acc_log2
     uint32_t persistent;     // kSched*: tile scheduling of this launch
     uint32_t flags;          // RT_FLAG_* diagnostic ablations

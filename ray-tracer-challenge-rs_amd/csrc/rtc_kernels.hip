@@ -1964,16 +1964,15 @@ __device__ inline void set_wave_prio(uint32_t p) {
 
 // Ray pool: one LIFO of pending rays per WORKGROUP, run in block-lockstep
 // generations (trace_pool).  Dynamic LDS after the world tables holds
-//   [acc: P.pool_slots (1, or 2 with item refill) x 3 x kBlock PoolAcc<R>:
-//    the open items' pixel sums]
+//   [acc: kTileSlots (1) x 3 x kBlock PoolAcc<R>: the tile's pixel sums]
 //   [ox oy oz dx dy dz w : lds_cap x R][meta : lds_cap x PoolMeta]
-// with meta = pixel | slot << 8 | remaining << 9 (pixel = the lane of its
-// item's 64x4 tile, 0..255; 14 bits, so 16-bit entries give the pool 1/16
-// more slots in the same LDS; rtc_internal.hpp PoolMeta).  Slots [lds_cap, cap) live in the
+// with meta = pixel | remaining << 8 (pixel = the lane of the 64x4 tile,
+// 0..255; 13 bits, so 16-bit entries give the pool 1/16 more slots in the
+// same LDS; rtc_internal.hpp PoolMeta).  Slots [lds_cap, cap) live in the
 // workgroup's region of P.spill, one 8-word record per entry (AoS: a lane's
 // entry is two dwordx4 stores / loads in f32, where the SoA layout took
 // eight dword instructions per entry; the record keeps meta in 32 bits).
-// The LIFO bound cap = kBlock (x 2 with refill) + depth x batch (rtc_host.cpp pool_capacity)
+// The LIFO bound cap = kBlock + depth x batch (rtc_host.cpp pool_capacity)
 // makes overflow impossible; the LDS part is sized for occupancy
 // (plan_launch), deep excursions spill.
 template <typename R>
@@ -2154,16 +2153,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     constexpr bool kDiag = true;
     if (kDiag && P.stamps && threadIdx.x == 0) P.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     unsigned char* smem = smem_all + (kLds ? P.world_lds : 0);
+    __shared__ unsigned int s_tile[2];
     __shared__ int s_top[2];
-    __shared__ int s_live[kPoolSlotsMax];           // rays of each open item in the pool
-    __shared__ unsigned int s_next[2];              // the next item from the queues (thread 0 fetches it)
-    __shared__ unsigned long long s_start[kPoolSlotsMax];  // thread 0: s_memrealtime when the item opened
     const uint32_t cap = P.pool_capacity;
     const uint32_t lcap = P.pool_lds_capacity, gcap = cap - lcap;
     Pool<R> pl;
     pl.acc = reinterpret_cast<PoolAcc<R>*>(smem);
-    const int nslots = (int)P.pool_slots;  // (launch-uniform: 1, or 2 with item refill)
-    pl.lds = reinterpret_cast<R*>(smem + (size_t)nslots * 3 * kBlock * sizeof(PoolAcc<R>));
+    pl.lds = reinterpret_cast<R*>(smem + 3 * kBlock * sizeof(PoolAcc<R>));
     const float acc_scale = __builtin_ldexpf(1.0f, (int)P.acc_log2);
     pl.lds_cap = (int)lcap;
     // 8 words per spilled entry; blockIdx.x < grid (persistent launch)
@@ -2184,200 +2180,107 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(sizeof(R
     uint32_t probe = 0;
     // thread 0: the items of this launch (read once: it sits on the dequeue path)
     const uint32_t n_items = P.item_count && tid == 0 ? *P.item_count : P.n_tiles;
-    uint32_t fetched = 0;  // thread 0: items taken from the queues so far
-    if (tid == 0) {
-        s_top[0] = 0;
-        for (int s = 0; s < kPoolSlotsMax; ++s) s_live[s] = 0;
-        s_next[0] = next_tile(P, fetched++, probe, n_items);
-    }
-    for (int i = (int)tid; i < nslots * 3 * kBlock; i += kBlock) pl.acc[i] = 0;
-    __syncthreads();
-    // The open items live in registers, the same in every thread (every
-    // thread opens and closes the same items in the same generations):
-    // item[s] of slot s, kNoItem when free.  Shared words are read only
-    // where no wave can be changing them: s_next alternates between two
-    // words (thread 0 fetches into the one not being read), the pool's top
-    // and the live counts are read after the barrier that completes their
-    // atomics and before the barrier after which they change.
-    uint32_t item[kPoolSlotsMax];
-    for (int s = 0; s < kPoolSlotsMax; ++s) item[s] = kNoItem;
-    uint32_t opens = 0, prio_now = 0;
-    const uint32_t lane = tid & 63u;
-    // Generations of the workgroup's LIFO.  An item (a tile, or a part of a
-    // split tile) opens into a free slot of accumulators by pushing its
-    // primary rays; its rays carry the slot in their meta, and it closes
-    // (its pixels are written) once none of them is left in the pool.  One
-    // item at a time, as rounds 1-5 ran, unless item refill is on
-    // (P.refill_below): then a second item opens while fewer rays than that
-    // are left to pop, so lanes a sparse generation would leave idle (the
-    // first generations of a split tile's part, the last ones of any tile)
-    // trace the next item's rays instead.
-    for (uint32_t gen = 0;; ++gen) {
-        const int cur = gen & 1;
+    unsigned long long tile_start = 0;  // thread 0: s_memrealtime at the tile's start
+    for (uint32_t it = 0;; ++it) {
+        if (tid == 0) {
+            s_tile[it & 1] = next_tile(P, it, probe, n_items);
+            s_top[0] = 0;
+            tile_start = __builtin_amdgcn_s_memrealtime();
+        }
+        for (int c = 0; c < 3; ++c) pl.acc[c * kBlock + tid] = 0;
+        __syncthreads();
+        const uint32_t item = __builtin_amdgcn_readfirstlane(s_tile[it & 1]);
+        if (item == kNoItem) break;
+        // packed fields only in items handed out through a tile order (raster
+        // items are plain tile indices, any number of them)
+        const WorkItem wi = decode_item(item, P.tile_order != nullptr);
+        const uint32_t t = wi.tile, split = wi.split_log2;
+#ifdef RTC_BOUNDS_CHECK
+        if (!in_bounds(t < P.n_tiles, P.error_flag, kErrBoundsTile)) continue;  // (every thread: uniform)
+#endif
+        // the costliest items set the launch's tail: their waves win issue
+        // arbitration against the other workgroups' on the same SIMDs
+        const uint32_t prio = wi.prio;
+        if (prio) set_wave_prio(prio);
+        bool valid;
+        V3<R> o, d;
+        uint64_t out_idx;
+        load_primary(P, t, tid, valid, o, d, out_idx);
+        // this item's part of the tile (all of it unless split)
+        valid &= item_seeds(tid, wi);
+        k.c[0] += wave_count(valid);
         {
-            const uint32_t next = __builtin_amdgcn_readfirstlane(s_next[opens & 1]);
-            int free_slot = -1, n_open = 0;
-            for (int s = 0; s < nslots; ++s) {
-                n_open += item[s] != kNoItem ? 1 : 0;
-                if (item[s] == kNoItem && free_slot < 0) free_slot = s;
-            }
-            if (next == kNoItem && n_open == 0) break;  // drained: every item written
-            bool open = false;
-            if (next != kNoItem && free_slot >= 0) {
-                if (n_open == 0) {
-                    open = true;  // (the pool is empty: every item closed)
-                } else if (P.refill_below) {
-                    // the pool's size, final since the generation's last barrier;
-                    // the seeds below change it only after every wave has read it
-                    open = __builtin_amdgcn_readfirstlane(s_top[cur]) < (int)P.refill_below;
-                    if (open) __syncthreads();
-                }
-            }
-            if (open) {
-                // packed fields only in items handed out through a tile order (raster
-                // items are plain tile indices, any number of them)
-                const WorkItem wi = decode_item(next, P.tile_order != nullptr);
-                bool valid = false;
-                V3<R> o, d;
-                uint64_t out_idx;
-#ifdef RTC_BOUNDS_CHECK
-                const bool tile_ok = in_bounds(wi.tile < P.n_tiles, P.error_flag, kErrBoundsTile);
-#else
-                constexpr bool tile_ok = true;
-#endif
-                if (tile_ok) load_primary(P, wi.tile, tid, valid, o, d, out_idx);
-                // this item's part of the tile (all of it unless split)
-                valid = tile_ok && valid && item_seeds(tid, wi);
-                const uint32_t seeds = wave_count(valid);
-                k.c[0] += seeds;
-                const int slot = wave_reserve(valid, &s_top[cur]);
-                if (valid)
-                    pool_put(pl, slot, o, d, (R)1,
-                             tid | ((uint32_t)free_slot << kMetaSlotShift) | (P.max_depth << kMetaRemShift));
-                if (lane == 0 && seeds) atomicAdd(&s_live[free_slot], (int)seeds);
-                if (tid == 0) {
-                    s_start[free_slot] = __builtin_amdgcn_s_memrealtime();
-                    s_next[(opens + 1) & 1] = next_tile(P, fetched++, probe, n_items);
-                }
-                item[free_slot] = next;
-                ++opens;
-                // the costliest items set the launch's tail: their waves win issue
-                // arbitration against the other workgroups' on the same SIMDs
-                if (wi.prio > prio_now) {
-                    prio_now = wi.prio;
-                    set_wave_prio(prio_now);
-                }
-                __syncthreads();  // seeds pushed and counted, the next item fetched
-            }
+            const int slot = wave_reserve(valid, &s_top[0]);
+            if (valid) pool_put(pl, slot, o, d, (R)1, tid | (P.max_depth << 8));
         }
-        const int size = s_top[cur];  // (0 when the items open have no pixel left in the canvas)
-        const int kpop = size < (int)P.pop_batch ? size : (int)P.pop_batch;
-        const int bottom = size - kpop;
-        const bool active = (int)tid < kpop;
-        V3<R> ro, rd;
-        R rw = (R)0;
-        uint32_t meta = 0;
-        if (active) pool_get(pl, bottom + (int)tid, ro, rd, rw, meta);
-        if (tid == 0) s_top[cur ^ 1] = bottom;
-        __syncthreads();  // every lane holds its ray; the next top is set
-        Shaded<R> sh;
-        bool hit = false;
-        const uint32_t pix = meta & 0xFFu;
-        const uint32_t rslot = (meta >> kMetaSlotShift) & 1u;
-        const uint32_t rem = meta >> kMetaRemShift;
-        const uint32_t child_meta = (meta & ((1u << kMetaRemShift) - 1u)) | ((rem - 1u) << kMetaRemShift);
-        uint32_t pushed = 0;
-        // lanes spawning a child reserve pool slots together (ballot +
-        // one LDS atomic per wave) at the point the child is made
-        auto push = [&](V3<R> co, V3<R> cd, R cw) {
-            const int slot = wave_reserve(true, &s_top[cur ^ 1]);
-            if (slot < (int)cap) {
-                pool_put(pl, slot, co, cd, rw * cw, child_meta);
-                ++pushed;
-            } else {
-                atomicOr(P.error_flag, kErrPoolOverflow);
-            }
-        };
-        if (active) hit = shade_ray<R, true, kDup>(sc, ro, rd, rem, sh, push);
-        count_events(k, false, hit, sh, sc.n_lights);
+        __syncthreads();
+        for (uint32_t gen = 0;; ++gen) {
+            const int cur = gen & 1;
+            const int size = s_top[cur];
+            if (size == 0) break;
+            const int kpop = size < (int)P.pop_batch ? size : (int)P.pop_batch;
+            const int bottom = size - kpop;
+            const bool active = (int)tid < kpop;
+            V3<R> ro, rd;
+            R rw = (R)0;
+            uint32_t meta = 0;
+            if (active) pool_get(pl, bottom + (int)tid, ro, rd, rw, meta);
+            if (tid == 0) s_top[cur ^ 1] = bottom;
+            __syncthreads();  // every lane holds its ray; the next top is set
+            Shaded<R> sh;
+            bool hit = false;
+            const uint32_t pix = meta & 0xFFu;
+            const uint32_t child_meta = pix | (((meta >> 8) - 1u) << 8);
+            // lanes spawning a child reserve pool slots together (ballot +
+            // one LDS atomic per wave) at the point the child is made
+            auto push = [&](V3<R> co, V3<R> cd, R cw) {
+                const int slot = wave_reserve(true, &s_top[cur ^ 1]);
+                if (slot < (int)cap) pool_put(pl, slot, co, cd, rw * cw, child_meta);
+                else atomicOr(P.error_flag, kErrPoolOverflow);
+            };
+            if (active) hit = shade_ray<R, true, kDup>(sc, ro, rd, meta >> 8, sh, push);
+            count_events(k, false, hit, sh, sc.n_lights);
 #ifndef RTC_JIT  // (per-scene builds never take RT_FLAG_GENERATIONS launches)
-        if (P.gen_counts) count_generations(P.gen_counts, active, hit, rem);
+            if (P.gen_counts) count_generations(P.gen_counts, active, hit, meta >> 8);
 #endif
-        if (hit) {
-            PoolAcc<R>* acc = pl.acc + rslot * (3 * kBlock);
-            acc_add(acc, pix, sh.surface.x * rw, acc_scale);
-            acc_add(acc + kBlock, pix, sh.surface.y * rw, acc_scale);
-            acc_add(acc + 2 * kBlock, pix, sh.surface.z * rw, acc_scale);
-        }
-        // each slot's live rays: -1 per ray traced, +1 per child stored (one
-        // LDS atomic per wave and slot)
-        for (int s = 0; s < nslots; ++s) {
-            const bool mine = active && rslot == (uint32_t)s;
-            const int delta = (int)wave_count(mine && pushed >= 1u) + (int)wave_count(mine && pushed >= 2u) -
-                              (int)wave_count(mine);
-            if (lane == 0 && delta) atomicAdd(&s_live[s], delta);
-        }
-        __syncthreads();  // pushes and counts complete before the next pop
-        // An overflow (never, by the bound; the error is flagged) drops the
-        // pool and closes the open items with what they have.
-        if (__builtin_amdgcn_readfirstlane(s_top[cur ^ 1]) > (int)cap) {
-            __syncthreads();
-            if (tid == 0) {
-                s_top[cur ^ 1] = 0;
-                for (int s = 0; s < kPoolSlotsMax; ++s) s_live[s] = 0;
+            if (hit) {
+                acc_add(pl.acc, pix, sh.surface.x * rw, acc_scale);
+                acc_add(pl.acc + kBlock, pix, sh.surface.y * rw, acc_scale);
+                acc_add(pl.acc + 2 * kBlock, pix, sh.surface.z * rw, acc_scale);
             }
-            __syncthreads();
+            __syncthreads();  // pushes complete before the next pop
+            if (s_top[cur ^ 1] > (int)cap) {  // overflowed: drop the pool (error already flagged)
+                __syncthreads();
+                if (tid == 0) s_top[cur ^ 1] = 0;
+                __syncthreads();
+            }
         }
-        // Close the items none of whose rays is left: write their pixels.
-        bool closed = false;
-        for (int s = 0; s < nslots; ++s) {
-            if (item[s] == kNoItem || __builtin_amdgcn_readfirstlane(s_live[s]) != 0) continue;
-            closed = true;
-            const WorkItem wi = decode_item(item[s], P.tile_order != nullptr);
-            const uint32_t t = wi.tile;
-            uint64_t out_idx = 0;
-            bool valid = t < P.n_tiles && item_pixel(P, t, tid, out_idx) && item_seeds(tid, wi);
-            PoolAcc<R>* acc = pl.acc + s * (3 * kBlock);
-            const double inv = sizeof(PoolAcc<R>) == 4 ? __builtin_ldexp(1.0, -(int)P.acc_log2) : kAccInvScale;
-            const V3<R> c = {(R)((double)acc[tid] * inv), (R)((double)acc[kBlock + tid] * inv),
-                             (R)((double)acc[2 * kBlock + tid] * inv)};
+        const double inv = sizeof(PoolAcc<R>) == 4 ? __builtin_ldexp(1.0, -(int)P.acc_log2) : kAccInvScale;
+        const V3<R> c = {(R)((double)pl.acc[tid] * inv), (R)((double)pl.acc[kBlock + tid] * inv),
+                         (R)((double)pl.acc[2 * kBlock + tid] * inv)};
 #ifdef RTC_BOUNDS_CHECK
-            valid &= in_bounds(!valid || out_idx < (P.rays ? P.n_rays
-                                                           : (uint64_t)(P.image_rows ? P.height : P.tile_rows * RT_TILE_H) *
-                                                                 P.width),
-                               P.error_flag, kErrBoundsOut);
+        valid &= in_bounds(!valid || out_idx < (P.rays ? P.n_rays
+                                                       : (uint64_t)(P.image_rows ? P.height : P.tile_rows * RT_TILE_H) *
+                                                             P.width),
+                           P.error_flag, kErrBoundsOut);
 #endif
-            if (valid) store_pixel(P, out_idx, c);
-            acc[tid] = 0;
-            acc[kBlock + tid] = 0;
-            acc[2 * kBlock + tid] = 0;
-            // this item's cost (10 ns ticks) orders the next launch of the same
-            // frame heaviest-first (order_tiles); a split tile: its slowest part
-            // times the parts (order_tiles zeroed it)
-            if (tid == 0 && P.tile_cost && t < P.n_tiles) {
-                const uint32_t cst = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - s_start[s], 0x0FFFFFFFull);
-                if (wi.split_log2) atomicMax(&P.tile_cost[t], cst << wi.split_log2);
-                else P.tile_cost[t] = cst;
-            }
-            if (kDiag && tid == 0 && P.item_log) {  // diagnostics (RT_FLAG_STAMPS): the item's span
-                const unsigned long long n = atomicAdd(&P.item_log[0], 1ull);
-                P.item_log[1 + 3 * n] = item[s] | (unsigned long long)blockIdx.x << 32;
-                P.item_log[2 + 3 * n] = s_start[s];
-                P.item_log[3 + 3 * n] = __builtin_amdgcn_s_memrealtime();
-            }
-            item[s] = kNoItem;
-            // wave priority: the highest of the items still open
-            uint32_t p = 0;
-            for (int q = 0; q < nslots; ++q)
-                if (item[q] != kNoItem) p = max(p, decode_item(item[q], P.tile_order != nullptr).prio);
-            if (p != prio_now) {
-                prio_now = p;
-                set_wave_prio(p);
-            }
+        if (valid) store_pixel(P, out_idx, c);
+        if (prio) __builtin_amdgcn_s_setprio(0);
+        __syncthreads();  // accumulators are re-zeroed for the next tile
+        // this tile's cost (10 ns ticks) orders the next launch of the same
+        // frame heaviest-first (order_tiles)
+        // (a split tile: its slowest part times the parts, order_tiles zeroed it)
+        if (tid == 0 && P.tile_cost) {
+            const uint32_t c = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - tile_start, 0x0FFFFFFFull);
+            if (split) atomicMax(&P.tile_cost[t], c << split);
+            else P.tile_cost[t] = c;
         }
-        // Every wave has read the live counts (and zeroed its accumulator
-        // entries) before an item opens into a freed slot.
-        if (closed) __syncthreads();
+        if (kDiag && tid == 0 && P.item_log) {  // diagnostics (RT_FLAG_STAMPS): the item's span
+            const unsigned long long k = atomicAdd(&P.item_log[0], 1ull);
+            P.item_log[1 + 3 * k] = item | (unsigned long long)blockIdx.x << 32;
+            P.item_log[2 + 3 * k] = tile_start;
+            P.item_log[3 + 3 * k] = __builtin_amdgcn_s_memrealtime();
+        }
     }
     if (!(P.flags & RT_FLAG_NO_COUNTERS)) flush_counts(k, P.counters);
     if (kDiag && P.stamps) {

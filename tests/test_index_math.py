@@ -5,8 +5,7 @@
   launches, plain tiles of any size in raster ones: ADVICE r3), the threads a
   split part seeds, spill record addressing, the row-block shard maps.
 * The LIFO bound the pool's capacity rests on (rtc_host.cpp pool_capacity:
-  kBlock + depth x batch, kBlock more with item refill): a model of
-  trace_pool's generation loop
+  kBlock + depth x batch): a model of trace_pool's generation loop
   (rtc_kernels.hip: pop the top min(size, 256) rays, push each popped ray's
   0-2 children with remaining - 1, in any order) never holds more.  This is
   the reference's recursion (world.rs:114-157: a shaded hit spawns at most a
@@ -66,48 +65,3 @@ def test_lifo_pool_bound(policy):
                 assert peak <= cap, (depth, seeds, peak, cap)
                 if policy == "both" and seeds == BLOCK:
                     assert peak == cap  # the bound is tight: every ray spawning both children
-
-
-def _refill_peak(depth, items, refill, rng, children, slots=2):
-    """trace_pool with item refill: an item opens (its seeds pushed at
-    `depth`) into a free slot when none is open, or while fewer than
-    `refill` rays are left; an item closes once none of its rays is left."""
-    stack, queue, live = [], list(items), {}
-    peak = 0
-    while queue or live:
-        if queue and len(live) < slots and (not live or len(stack) < refill):
-            slot = next(s for s in range(slots) if s not in live)
-            n = queue.pop(0)
-            stack += [(depth, slot)] * n
-            live[slot] = n
-            peak = max(peak, len(stack))
-        k = min(len(stack), BLOCK)
-        popped = stack[-k:] if k else []
-        del stack[len(stack) - k:]
-        kids = []
-        for rem, slot in popped:
-            live[slot] -= 1
-            if rem > 0:
-                c = children(rng)
-                kids += [(rem - 1, slot)] * c
-                live[slot] += c
-        rng.shuffle(kids)
-        stack += kids
-        peak = max(peak, len(stack))
-        for slot in [s for s, n in live.items() if n == 0]:
-            del live[slot]
-    return peak
-
-
-@pytest.mark.parametrize("policy", ["both", "random", "mostly_both"])
-def test_lifo_pool_bound_with_refill(policy):
-    children = {"both": lambda r: 2, "random": lambda r: r.choice((0, 1, 2)),
-                "mostly_both": lambda r: r.choice((0, 1, 2, 2, 2))}[policy]
-    rng = random.Random(11)
-    for depth in range(0, 9):
-        cap = 2 * BLOCK + depth * BLOCK
-        for refill in (64, 128, 256):
-            for _ in range(2 if policy == "both" else 6):
-                items = [rng.choice((16, 32, 64, 128, 256)) for _ in range(rng.randint(1, 12))]
-                peak = _refill_peak(depth, items, refill, rng, children)
-                assert peak <= cap, (depth, items, refill, peak, cap)
