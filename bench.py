@@ -371,7 +371,7 @@ def main():
                     "value", "unit", "ms_per_step", "steps", "scaling", "config", "render_ms_per_shard",
                     "gather_ms", "frame_ms", "gather", "gather_variants", "single_gpu_ms_per_step",
                     "speedup_vs_1gpu", "strong_scaling_efficiency", "single_gpu_value", "roofline",
-                    "first_frame_ms", "device_state") if k in split}
+                    "first_frame_ms", "device_state", "shards_of_8_on_one_gpu") if k in split}
         if rank == 0:
             line["scaling_note"] = (
                 "value: N independent configs[1] frames per step, one per GPU (weak scaling: a throughput check, "
@@ -583,6 +583,25 @@ def measure(args, tiled, world, rank, local):
                 # denominator for this line's scaling (the default N=1 line is
                 # configs[1], three_sphere at 1080p, a different workload)
                 extra["single_gpu_value"] = total_rays / args.steps / (single_ms * 1e-3) / 1e6
+                # the 8-way split on this one GPU: each shard's kernel ms (what
+                # rank r renders at N = 8; warm, cost-ordered, median of 3), so
+                # every line carries the slowest of 8 beside its own split
+                rows8 = rtc_amd.shard_rows(cam.height, 8)
+                strip8 = torch.empty((rows8, cam.width, 3), dtype=rdtype, device="cuda")
+                per8 = []
+                for kk in range(8):
+                    f8 = lambda: one.render_device(cam, strip8.data_ptr(), sptr, args.depth,  # noqa: E731
+                                                   args.precision, args.out, (kk, 8))
+                    for _ in range(3):
+                        f8()
+                    torch.cuda.synchronize()
+                    per8.append(float(np.median([timed_launches(f8, stream, 1)() for _ in range(3)])))
+                whole1 = float(np.median([timed_launches(f1, stream, 1)() for _ in range(3)]))
+                extra["shards_of_8_on_one_gpu"] = {
+                    "kernel_ms": [round(x, 4) for x in per8], "slowest_ms": max(per8),
+                    "whole_frame_ms": whole1, "sum_over_whole": sum(per8) / whole1,
+                    "note": "each row-block shard of the 8-way split rendered alone on rank 0's GPU (the render "
+                            "time of each rank at N = 8, before the gather)"}
         if world > 1:
             dist.barrier()
     else:
@@ -595,8 +614,15 @@ def measure(args, tiled, world, rank, local):
         workload = f"{args.scene}@{cam.width}x{cam.height},depth={args.depth},{args.precision}"
         if args.out == "u8":
             workload += ",u8"
-        traffic = load_profile("traffic.json", workload) if not tiled else None
-        issue = (load_profile("issue.json", workload) or {}) if not tiled else {}
+        if tiled:
+            # the tile split's PMC figures (scripts/shard_pmc.sh): the whole frame at
+            # N = 1, one of the eight shards a rank renders at N = 8, none otherwise
+            split_prof = load_profile("tile_split_pmc.json", workload + (f",shard_of_{world}" if world > 1 else ""))
+            traffic = (split_prof or {}).get("traffic")
+            issue = split_prof or {}
+        else:
+            traffic = load_profile("traffic.json", workload)
+            issue = load_profile("issue.json", workload) or {}
         line = {
             "metric": "Mray/s (primary+secondary) and ms/frame at 1920x1080",
             "value": total_rays / elapsed / 1e6,
