@@ -358,7 +358,9 @@ def main():
     # split across the N GPUs by librtc's RCCL group) and attaches it as
     # "tile_split"; --mode tiled makes that split the line itself.
     tiled = args.mode == "tiled"
-    line = measure(resolve(args, tiled), tiled, world, rank, local)
+    # the device state before anything runs (measure: why not next to the region)
+    state0 = device_state(local)
+    line = measure(resolve(args, tiled), tiled, world, rank, local, state0)
     if args.mode == "auto":
         # The north star's strong-scaling series, at every N (N = 1 included,
         # so a scaling curve compares one workload): configs[3] and configs[4],
@@ -399,7 +401,7 @@ def args_for_split(args, scene):
     return a
 
 
-def measure(args, tiled, world, rank, local):
+def measure(args, tiled, world, rank, local, state_before=None):
     """One workload on this rank's GPU (frames) or split across the group
     (tiled); returns rank 0's JSON line (None elsewhere)."""
     import numpy as np
@@ -412,9 +414,11 @@ def measure(args, tiled, world, rank, local):
     # The device state before anything of this workload runs: an amdsmi query
     # next to the timed region slowed its frames by 20 % (round 6, same box,
     # three_sphere 1080p: 15.7 -> 18.8 us per frame with a sample right
-    # before the region), so the samples are taken here, ahead
-    # of the >= 200 ms warm-up, and after the region's clock has stopped.
-    state_before = device_state(local)
+    # before the region), so the samples are taken before the
+    # context, the first frame and the >= 200 ms warm-up, and after the
+    # region's clock has stopped.
+    if state_before is None:
+        state_before = device_state(local)
     # Only rank 0 holds the world, as the reference's single caller does
     t_first = time.perf_counter()
     scene = scene_io.load(os.path.join(ROOT, "tests", "golden", "scenes", f"{args.scene}.json")) if rank == 0 else None
