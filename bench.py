@@ -81,6 +81,10 @@ def parse():
                          "measured too and reported under gather_variants")
     ap.add_argument("--ab", action="store_true",
                     help="A/B runs: skip the one-shot child, the host-frame latency and the per-generation frame")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="frames in flight: consecutive steps alternate between this many contexts, each on a "
+                         "stream of its own, so one frame's launch tail overlaps the next frame's start (1 = "
+                         "every frame on one stream, one after another)")
     ap.add_argument("--stream", choices=["side", "null"], default="side",
                     help="the launch stream: a stream of the bench's own (default) or HIP's null stream")
     ap.add_argument("--one-shot-child", action="store_true", help=argparse.SUPPRESS)
@@ -232,21 +236,32 @@ def _power(info: dict):
 
 
 def timed_launches(fn, stream, n):
-    """Device milliseconds of n back-to-back calls of fn(), one event pair on `stream`.
-    The events are created (torch makes the HIP event at its first record) and
-    recorded once before the caller's clock starts: a lazy hipEventCreate inside
-    a 20-frame region added ~70 us to it (scripts/short_region_probe.py)."""
+    """Device milliseconds of n back-to-back calls of fn(), one event pair on
+    `stream` (a list: the first stream opens the bracket, the others join its
+    start and are joined back before it closes).  The events are created
+    (torch makes the HIP event at its first record) and recorded once before
+    the caller's clock starts: a lazy hipEventCreate inside a 20-frame region
+    added ~70 us to it (scripts/short_region_probe.py)."""
     import torch
+    streams = stream if isinstance(stream, (list, tuple)) else [stream]
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    e1.record(stream)
+    joins = [torch.cuda.Event() for _ in streams[1:]]
+    e0.record(streams[0])
+    e1.record(streams[0])
+    for j, s in zip(joins, streams[1:]):
+        j.record(s)
     torch.cuda.synchronize()
 
     def run():
-        e0.record(stream)
+        e0.record(streams[0])
+        for s in streams[1:]:
+            s.wait_event(e0)
         for _ in range(n):
             fn()
-        e1.record(stream)
+        for j, s in zip(joins, streams[1:]):
+            j.record(s)
+            streams[0].wait_event(j)
+        e1.record(streams[0])
         torch.cuda.synchronize()
         return e0.elapsed_time(e1)
     return run
@@ -426,44 +441,79 @@ def measure(args, tiled, world, rank, local, state_before=None):
     # the frames run on a stream of their own (HIP's null stream orders every
     # launch against the device's other blocking streams; --stream null keeps
     # it for the A/B)
-    stream = torch.cuda.Stream() if args.stream == "side" else torch.cuda.current_stream()
+    # Frames in flight (--inflight F): consecutive steps alternate between F
+    # contexts, each with its own stream and output buffer, so a frame's
+    # launch tail (its last workgroups) overlaps the next frame's first
+    # ones.  Round 6, same box (scripts/overlap_probe.py): three_sphere 1080p
+    # 15.65 -> 12.59 us per frame, a cover 4K shard of 8 0.125 -> 0.103 ms,
+    # table's 0.141 -> 0.114, reflect_refract 0.236 -> 0.220; frames equal.
+    # Each frame is whole and independent (a context renders it from its own
+    # resident scene copy), as a renderer producing an animation would run.
+    inflight = max(1, args.inflight)
+    # the frames run on streams of their own (HIP's null stream orders every
+    # launch against the device's other blocking streams; --stream null keeps
+    # it for the A/B, with one frame in flight)
+    if args.stream == "null":
+        inflight = 1
+    streams = [torch.cuda.Stream() if args.stream == "side" else torch.cuda.current_stream() for _ in range(inflight)]
+    stream = streams[0]
     sptr = stream.cuda_stream
     rdtype = torch.uint8 if args.out == "u8" else (torch.float32 if args.precision == "f32" else torch.float64)
     if tiled:
         # the library's multi-GPU context: RCCL communicator from a unique id,
         # scene broadcast inside rt_scene_upload, strips gathered onto rank 0
-        uid = rdist.share_unique_id(rank) if world > 1 else rtc_amd.comm_unique_id()
+        # (one group per frame in flight: each its own communicator)
+        uids = [rdist.share_unique_id(rank) if world > 1 else rtc_amd.comm_unique_id() for _ in range(inflight)]
         t = time.perf_counter()
-        ctx = rtc_amd.Context.rank(local, world, rank, uid)
-        ctx.set_gather(rtc_amd.RT_GATHER_PEER if args.gather == "peer" else rtc_amd.RT_GATHER_RCCL)
+        ctxs = [rtc_amd.Context.rank(local, world, rank, u) for u in uids]
+        for c in ctxs:
+            c.set_gather(rtc_amd.RT_GATHER_PEER if args.gather == "peer" else rtc_amd.RT_GATHER_RCCL)
         phase["context_ms"] = (time.perf_counter() - t) * 1e3
         t = time.perf_counter()
         # every rank raises if any rank's part of the upload failed (no rank
         # left waiting in the next collective: rdist.collective_call)
-        rdist.collective_call(lambda: ctx.upload(scene if rank == 0 else None), rank)
+        for c in ctxs:
+            rdist.collective_call(lambda: c.upload(scene if rank == 0 else None), rank)
         phase["upload_ms"] = (time.perf_counter() - t) * 1e3
         cam0 = rtc_amd.camera_resize(scene.camera, args.width, args.height) if rank == 0 else None
         cam = rdist.share_camera(cam0, rank) if world > 1 else cam0
-        image = torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda") if rank == 0 else None
-        out_ptr = image.data_ptr() if rank == 0 else None
+        images = [torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda") if rank == 0 else None
+                  for _ in range(inflight)]
     else:
         if world > 1:
             scene = rdist.broadcast_scene(scene, rank, "cpu")
         cam = rtc_amd.camera_resize(scene.camera, args.width, args.height)
         t = time.perf_counter()
-        ctx = rtc_amd.Context(local)
+        ctxs = [rtc_amd.Context(local) for _ in range(inflight)]
         phase["context_ms"] = (time.perf_counter() - t) * 1e3
         t = time.perf_counter()
-        ctx.upload(scene)
+        for c in ctxs:
+            c.upload(scene)
         phase["upload_ms"] = (time.perf_counter() - t) * 1e3
-        image = torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda")
-        out_ptr = image.data_ptr()
+        images = [torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda") for _ in range(inflight)]
+    ctx, image = ctxs[0], images[0]
+    out_ptrs = [im.data_ptr() if im is not None else None for im in images]
+    sptrs = [s_.cuda_stream for s_ in streams]
+    turn = [0]
 
-    def step():
-        ctx.render_device(cam, out_ptr, sptr, args.depth, args.precision, args.out, (0, 1), args.flags)
+    def step_on(i):
+        ctxs[i].render_device(cam, out_ptrs[i], sptrs[i], args.depth, args.precision, args.out, (0, 1), args.flags)
+
+    def step():  # the next frame, round robin over the frames in flight
+        i = turn[0]
+        turn[0] = (i + 1) % inflight
+        step_on(i)
+
+    def step0():  # one frame on the first context (latency, cold launches)
+        step_on(0)
+
+    def counters_sum():
+        cs = [c.counters() for c in ctxs]
+        return {k: sum(c_[k] for c_ in cs) for k in ("rays", "algorithmic_flops", "primary", "shadow", "reflect",
+                                                      "refract")}
 
     t = time.perf_counter()
-    step()  # first frame: scene transfer, context, upload and one render
+    step0()  # first frame: scene transfer, context, upload and one render
     torch.cuda.synchronize()
     phase["first_render_ms"] = (time.perf_counter() - t) * 1e3
     first_frame_ms = (time.perf_counter() - t_first) * 1e3
@@ -476,8 +526,12 @@ def measure(args, tiled, world, rank, local, state_before=None):
     # frames switch once it lands.  The bench lets it land before the warm-up
     # so the timed region measures the steady-state kernel (untimed, reported).
     t_j = time.perf_counter()
-    step()
+    step0()
     jit_pending = ctx.jit_wait(120000.0)
+    for i in range(1, inflight):  # (the others find the landed build at their second frame)
+        step_on(i)
+        step_on(i)
+        jit_pending += ctxs[i].jit_wait(120000.0)
     jit_wait_ms = (time.perf_counter() - t_j) * 1e3
     # W untimed steps, continued (still untimed) until --warmup-ms of frames
     # have run: on MI355X a 1080p frame after 5 warm-up frames takes 24.6 us
@@ -505,7 +559,7 @@ def measure(args, tiled, world, rank, local, state_before=None):
     # on MI355X — they stop the next launch's waves from overlapping the
     # previous one's tail — see scripts/host_overhead.py): average = bracket / K.
     # Tiled: the bracket is rank 0's stream (its shard, the gather, the de-interleave).
-    timed = timed_launches(step, stream, args.steps)
+    timed = timed_launches(step, streams, args.steps)
     # The GPU should not sit idle between the warm-up and the timed region
     # (the events and the barrier above cost milliseconds): ~2 ms of untimed
     # frames keep it busy across them; the region itself is unchanged.
@@ -515,7 +569,8 @@ def measure(args, tiled, world, rank, local, state_before=None):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    before = ctx.counters()  # (a few-us copy: the region's rays are after - before)
+    turn[0] = 0
+    before = counters_sum()  # (a few-us copy per context: the region's rays are after - before)
     t0 = time.perf_counter()
     launch_ms = timed() / args.steps  # ends with torch.cuda.synchronize()
     # each rank's clock stops at its own synchronize; the closing barrier is
@@ -526,7 +581,7 @@ def measure(args, tiled, world, rank, local, state_before=None):
     state_after = device_state(local)
     if world > 1:
         dist.barrier()
-    after = ctx.counters()
+    after = counters_sum()
 
     rays = after["rays"] - before["rays"]
     flops = after["algorithmic_flops"] - before["algorithmic_flops"]
@@ -548,8 +603,9 @@ def measure(args, tiled, world, rank, local, state_before=None):
         variants = {args.gather: {"ms_per_step": elapsed * 1e3 / args.steps, "frame_ms": extra["frame_ms"],
                                   "gather_ms": extra["gather_ms"], "render_ms_per_shard": kernel_ms}}
         other = "peer" if args.gather == "rccl" else "rccl"
-        ctx.set_gather(rtc_amd.RT_GATHER_PEER if other == "peer" else rtc_amd.RT_GATHER_RCCL)
-        for _ in range(3):
+        for c in ctxs:
+            c.set_gather(rtc_amd.RT_GATHER_PEER if other == "peer" else rtc_amd.RT_GATHER_RCCL)
+        for _ in range(3 * inflight):
             step()
         torch.cuda.synchronize()
         if world > 1:
@@ -562,21 +618,35 @@ def measure(args, tiled, world, rank, local, state_before=None):
                            "frame_ms": float(np.median([st["frame_ms"] for st in sts2])),
                            "gather_ms": float(np.median([st["gather_ms"] for st in sts2])),
                            "render_ms_per_shard": float(np.median([st["kernel_ms"] for st in sts2]))}
-        ctx.set_gather(rtc_amd.RT_GATHER_PEER if args.gather == "peer" else rtc_amd.RT_GATHER_RCCL)
+        for c in ctxs:
+            c.set_gather(rtc_amd.RT_GATHER_PEER if args.gather == "peer" else rtc_amd.RT_GATHER_RCCL)
         extra["gather_variants"] = variants
         if world > 1:
             dist.barrier()
         if rank == 0:
-            # the same workload on rank 0's GPU alone (a single-GPU context)
-            with rtc_amd.Context(local) as one:
-                one.upload(scene)
-                full = torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda")
-                f1 = lambda: one.render_device(cam, full.data_ptr(), sptr, args.depth, args.precision,  # noqa: E731
-                                               args.out)
-                for _ in range(max(2, args.warmup)):
-                    f1()
+            # the same workload on rank 0's GPU alone (single-GPU contexts,
+            # the same frames in flight)
+            ones = [rtc_amd.Context(local) for _ in range(inflight)]
+            try:
+                for o_ in ones:
+                    o_.upload(scene)
+                one = ones[0]
+                fulls = [torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda") for _ in ones]
+                full = fulls[0]
+                turn1 = [0]
+
+                def f1_on(i):
+                    ones[i].render_device(cam, fulls[i].data_ptr(), sptrs[i], args.depth, args.precision, args.out)
+
+                def f1n():
+                    i = turn1[0]
+                    turn1[0] = (i + 1) % inflight
+                    f1_on(i)
+                f1 = lambda: f1_on(0)  # noqa: E731
+                for _ in range(max(2, args.warmup) * inflight):
+                    f1n()
                 torch.cuda.synchronize()
-                timed1 = timed_launches(f1, stream, args.steps)
+                timed1 = timed_launches(f1n, streams, args.steps)
                 t1 = time.perf_counter()
                 timed1()
                 single_ms = (time.perf_counter() - t1) * 1e3 / args.steps
@@ -606,8 +676,21 @@ def measure(args, tiled, world, rank, local, state_before=None):
                     "whole_frame_ms": whole1, "sum_over_whole": sum(per8) / whole1,
                     "note": "each row-block shard of the 8-way split rendered alone on rank 0's GPU (the render "
                             "time of each rank at N = 8, before the gather)"}
+            finally:
+                for o_ in ones:
+                    o_.close()
         if world > 1:
             dist.barrier()
+    elif inflight > 1:
+        # The roofline's per-launch duration: the same frames one after
+        # another on one stream (the K-frame bracket above overlaps frames in
+        # flight, so bracket / K is the throughput, not a launch's duration;
+        # rocprofv3's average duration agrees with this one).
+        lat = timed_launches(step0, [streams[0]], args.steps)
+        for _ in range(burst):
+            step0()
+        torch.cuda.synchronize()
+        kernel_ms = lat() / args.steps
     else:
         kernel_ms = launch_ms
     line = None
@@ -635,6 +718,10 @@ def measure(args, tiled, world, rank, local, state_before=None):
             "steps": args.steps,
             "warmup": args.warmup,
             "warmup_frames_run": warm_run,
+            "frames_in_flight": inflight,
+            # one frame's device time on its own (frames: one launch after another on
+            # one stream; tiled: rank 0's render + gather + de-interleave of one frame)
+            "frame_latency_ms": extra.get("frame_ms", kernel_ms) if tiled else kernel_ms,
             "rewarm_frames": burst,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
@@ -687,7 +774,7 @@ def measure(args, tiled, world, rank, local, state_before=None):
                 cold = []
                 for _ in range(3):
                     ctx.upload(scene)
-                    cold.append(timed_launches(step, stream, 1)())
+                    cold.append(timed_launches(step0, stream, 1)())
                 line["cold_kernel_ms"] = float(np.median(cold))
         if not tiled and world == 1 and not args.ab:
             # a drop-in Camera::render: synchronous rt_render into host memory,
@@ -740,7 +827,8 @@ def measure(args, tiled, world, rank, local, state_before=None):
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(scene, cam, args.depth, args.cpu_seconds)
             line["cpu_baseline"]["configs0_serial"] = cpu_serial_configs0(min(3.0, args.cpu_seconds / 4))
-    ctx.close()
+    for c in ctxs:
+        c.close()
     return line if rank == 0 else None
 
 
