@@ -15,7 +15,7 @@ rm -rf gpurun_out/${ROUND}_stats_* gpurun_out/${ROUND}_pmc_*
 echo "profile set ok"
 bash scripts/round_bench.sh > gpurun_out/${ROUND}_bench.log 2>&1 || { echo "bench lines failed"; exit 1; }
 echo "bench lines ok"
-{ SHARD_COUNTS=1,8 timeout -k 10 180 python scripts/shard_times.py cover 3840 2160 &&
-  SHARD_COUNTS=1,8 timeout -k 10 180 python scripts/shard_times.py table 3840 2160; } > gpurun_out/${ROUND}_shard_times.txt 2>&1 || { echo "shard times failed"; exit 1; }
+{ SHARD_INFLIGHT=2 SHARD_COUNTS=1,8 timeout -k 10 180 python scripts/shard_times.py cover 3840 2160 &&
+  SHARD_INFLIGHT=2 SHARD_COUNTS=1,8 timeout -k 10 180 python scripts/shard_times.py table 3840 2160; } > gpurun_out/${ROUND}_shard_times.txt 2>&1 || { echo "shard times failed"; exit 1; }
 du -sh gpurun_out
 echo "all ok"
