@@ -8,6 +8,6 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for ctrs in "${@}"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $ctrs -d $OUT/p$i -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 3 --warmup-ms 0 --no-cpu-baseline --ab --mode frames ${BENCH_ARGS:-} > $OUT/p$i.log 2>&1 || exit $?
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $ctrs -d $OUT/p$i -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 3 --warmup-ms 0 --no-cpu-baseline --ab --mode frames --inflight 1 ${BENCH_ARGS:-} > $OUT/p$i.log 2>&1 || exit $?
   echo "pass $i ($ctrs) ok"
 done
