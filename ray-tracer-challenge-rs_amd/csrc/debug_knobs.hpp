@@ -3,6 +3,7 @@
 //   RTC_DEBUG=cull=0,tile_order=0,split=0.5 python bench.py --ab
 // Product runs set none of them.  Keys (defaults in rtc_context.hpp):
 //   sched_direct=grid|static      direct-kernel tile scheduling
+//   direct_oversub=T              f32 direct kernel's grid: T/10 x the resident workgroups (default 25)
 //   lds_world=0                   world tables not staged in LDS
 //   cull=0                        every shape uploaded unbounded (no wave cull)
 //   kind_variants=0               no sphere/plane-only pool kernel

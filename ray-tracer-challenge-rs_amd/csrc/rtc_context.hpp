@@ -92,6 +92,8 @@ struct rt_context {
     // (RTC_DEBUG=sched_direct=grid|static; the pool kernel always takes the
     // per-XCD queues)
     uint32_t sched_direct = rtc::kSchedStatic;
+    // f32 direct kernel's resident-grid multiple, in tenths (RTC_DEBUG=direct_oversub=T)
+    uint32_t direct_oversub10 = 25;
     bool lds_world = true;      // RTC_DEBUG=lds_world=0 gathers shade data from global memory
     bool cull = true;  // RTC_DEBUG=cull=0 uploads every shape as unbounded (no wave cull; exactness tests)
     bool kind_variants = true;  // RTC_DEBUG=kind_variants=0: always the all-kinds kernels

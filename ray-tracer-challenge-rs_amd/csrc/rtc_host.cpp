@@ -585,7 +585,7 @@ int plan_launch(rt_context* ctx, const DevScene<R>& sc, uint32_t depth, uint32_t
     // 8160 (one tile each) 34.1 / 39.8; three_sphere 4K 115.6 -> 107.0 us.
     // The f64 kernel (3 waves/SIMD) measured 3.7% slower that way.
     const bool oversub = !ls.pool && ls.sched == kSchedStatic && sizeof(R) == 4;
-    const uint64_t grid_cap = oversub ? resident * 5 / 2 : resident;
+    const uint64_t grid_cap = oversub ? std::max<uint64_t>(1, resident * ctx->direct_oversub10 / 10) : resident;
     ls.grid = ls.sched != kSchedGrid ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, grid_cap)) : n_tiles;
     ls.grid_tiles = n_tiles;
     return RT_OK;
@@ -1027,6 +1027,7 @@ int create_device_context(int device_ordinal, rt_context** out) {
     if (debug_knob("split_max", &v))
         ctx->split_max = (uint32_t)std::min<int>((int)kMaxSplitLog2, std::max(0, std::atoi(v.c_str())));
     if (debug_knob("urgent", &v)) ctx->urgent_factor = std::atof(v.c_str());
+    if (debug_knob("direct_oversub", &v)) ctx->direct_oversub10 = (uint32_t)std::max(1, std::atoi(v.c_str()));
     // RTC_JIT: the per-scene build mode (rt_context_set_jit's values), a user setting
     if (const char* e = std::getenv("RTC_JIT"))
         ctx->jit_mode = (e[0] >= '0' && e[0] <= '3' && !e[1]) ? e[0] - '0' : RT_JIT_AUTO;
