@@ -491,6 +491,9 @@ def measure(args, tiled, world, rank, local, state_before=None):
             c.upload(scene)
         phase["upload_ms"] = (time.perf_counter() - t) * 1e3
         images = [torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda") for _ in range(inflight)]
+    if inflight > 1:  # (rtc.h planning hint: the direct kernel's grid for throughput)
+        for c in ctxs:
+            c.set_frames_in_flight(inflight)
     ctx, image = ctxs[0], images[0]
     out_ptrs = [im.data_ptr() if im is not None else None for im in images]
     sptrs = [s_.cuda_stream for s_ in streams]
@@ -630,6 +633,8 @@ def measure(args, tiled, world, rank, local, state_before=None):
             try:
                 for o_ in ones:
                     o_.upload(scene)
+                    if inflight > 1:
+                        o_.set_frames_in_flight(inflight)
                 one = ones[0]
                 fulls = [torch.empty((cam.height, cam.width, 3), dtype=rdtype, device="cuda") for _ in ones]
                 full = fulls[0]

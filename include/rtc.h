@@ -344,6 +344,16 @@ int rt_debug_normal(rt_context* ctx, uint32_t shape, const double* points, uint6
  * (default $XDG_CACHE_HOME/rtc_jit, else ~/.cache/rtc_jit). */
 enum { RT_JIT_OFF = 0, RT_JIT_SYNC = 1, RT_JIT_AUTO = 2, RT_JIT_EAGER = 3 };
 int rt_context_set_jit(rt_context* ctx, int mode);
+
+/* A planning hint: the caller keeps `frames` frames in flight (consecutive
+ * frames alternating between that many contexts, each on a stream of its
+ * own, so one frame's launch tail overlaps the next frame's start;
+ * INTEGRATION.md §2).  1 (the default) plans each launch for its own
+ * latency; > 1 plans the f32 direct kernel's grid for throughput (1.5x the
+ * resident workgroups instead of 2.5x: round 6, three_sphere 1080p with two
+ * in flight 339 -> 355-361 Gray/s, one frame alone 15.5 -> 16.1 us).  Pixels
+ * and rt_stats are unchanged.  Applies to every member of a group. */
+int rt_context_set_frames_in_flight(rt_context* ctx, uint32_t frames);
 int rt_jit_status(rt_context* ctx, int* used_last_launch, double* compile_ms, char* log, size_t log_len);
 int rt_jit_wait(rt_context* ctx, double timeout_ms, int* pending);
 

@@ -1617,6 +1617,16 @@ int rt_debug_normal(rt_context* ctx, uint32_t shape, const double* points, uint6
     return debug_shape(ctx, shape, 1, points, 3, n, precision, world_space, out, 3);
 }
 
+int rt_context_set_frames_in_flight(rt_context* ctx, uint32_t frames) {
+    if (!ctx || frames < 1) return set_error(RT_ERR_INVALID, "bad arguments");
+    std::string v;
+    const bool knob = debug_knob("direct_oversub", &v);  // (an A/B setting wins)
+    if (knob) return RT_OK;
+    ctx->direct_oversub10 = frames > 1 ? 15u : 25u;
+    for (rt_context* p : ctx->peers) p->direct_oversub10 = ctx->direct_oversub10;
+    return RT_OK;
+}
+
 int rt_context_set_jit(rt_context* ctx, int mode) {
     if (!ctx || mode < RT_JIT_OFF || mode > RT_JIT_EAGER) return set_error(RT_ERR_INVALID, "bad arguments");
     ctx->jit_mode = mode;

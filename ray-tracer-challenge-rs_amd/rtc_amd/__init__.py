@@ -199,6 +199,7 @@ def _load() -> C.CDLL:
         "rt_context_create_rank": (C.c_int, [C.c_int, C.c_int, C.c_int, P(C.c_uint8), P(C.c_void_p)]),
         "rt_context_group": (C.c_int, [C.c_void_p, P(C.c_int), P(C.c_int), P(C.c_int)]),
         "rt_context_set_jit": (C.c_int, [C.c_void_p, C.c_int]),
+        "rt_context_set_frames_in_flight": (C.c_int, [C.c_void_p, C.c_uint32]),
         "rt_jit_status": (C.c_int, [C.c_void_p, P(C.c_int), P(C.c_double), C.c_char_p, C.c_size_t]),
         "rt_jit_wait": (C.c_int, [C.c_void_p, C.c_double, P(C.c_int)]),
         "rt_canvas_create": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, P(C.c_void_p), P(C.c_uint8)]),
@@ -233,7 +234,7 @@ EXPORTED_SYMBOLS = (
     "rt_read_generation_counts",
     "rt_debug_stamps", "rt_debug_tile_costs", "rt_debug_item_log", "rt_debug_intersect", "rt_debug_normal", "rt_camera_set_transform",
     "rt_shard_row_map", "rt_context_create_multi", "rt_comm_unique_id", "rt_context_create_rank", "rt_context_group",
-    "rt_context_set_jit", "rt_jit_status", "rt_jit_wait", "rt_canvas_create", "rt_canvas_open", "rt_canvas_close",
+    "rt_context_set_jit", "rt_context_set_frames_in_flight", "rt_jit_status", "rt_jit_wait", "rt_canvas_create", "rt_canvas_open", "rt_canvas_close",
     "rt_render_to_canvas", "rt_canvas_wait", "rt_canvas_release", "rt_canvas_read", "rt_context_set_gather",
     "rt_assemble_shards", "rt_scene_load_yaml", "rt_scene_load_yaml_text", "rt_scene_view_get", "rt_scene_free",
     "rt_camera_make", "rt_camera_resize", "rt_matrix_inverse", "rt_image_write", "rt_image_write_format",
@@ -438,6 +439,11 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def set_frames_in_flight(self, frames: int) -> None:
+        """Planning hint (rtc.h rt_context_set_frames_in_flight): the caller keeps `frames` frames in
+        flight on as many contexts; > 1 plans the direct kernel for throughput.  Pixels unchanged."""
+        _check(_lib.rt_context_set_frames_in_flight(self._h, frames))
 
     def set_jit(self, mode: int) -> None:
         """Per-scene kernels (rtc.h rt_context_set_jit): 0 never, 1 every f32 frame (built in line),

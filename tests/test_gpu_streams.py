@@ -49,6 +49,8 @@ def test_frames_in_flight_on_two_contexts(rtc, name):
         for c in ctxs:
             c.upload(scene)
         ref, st = ctxs[0].render(cam, 6, precision="f32")
+        for c in ctxs:  # the planning hint (a throughput grid for the direct kernel): same frames
+            c.set_frames_in_flight(2)
         streams = [torch.cuda.Stream() for _ in ctxs]
         outs = [torch.empty((cam.height, cam.width, 3), dtype=torch.float32, device="cuda") for _ in ctxs]
         before = [c.counters()["rays"] for c in ctxs]
