@@ -351,8 +351,11 @@ int rt_context_set_jit(rt_context* ctx, int mode);
  * INTEGRATION.md §2).  1 (the default) plans each launch for its own
  * latency; > 1 plans the f32 direct kernel's grid for throughput (1.5x the
  * resident workgroups instead of 2.5x: round 6, three_sphere 1080p with two
- * in flight 339 -> 355-361 Gray/s, one frame alone 15.5 -> 16.1 us).  Pixels
- * and rt_stats are unchanged.  Applies to every member of a group. */
+ * in flight 339 -> 355-361 Gray/s, one frame alone 15.5 -> 16.1 us) and
+ * splits the pool kernels' heavy tiles only above 1.5x the mean workgroup
+ * load instead of 1x (a 4K shard of 8 with two in flight: cover 0.104 ->
+ * 0.094 ms).  Pixels and rt_stats are unchanged.  Applies to every member of
+ * a group. */
 int rt_context_set_frames_in_flight(rt_context* ctx, uint32_t frames);
 int rt_jit_status(rt_context* ctx, int* used_last_launch, double* compile_ms, char* log, size_t log_len);
 int rt_jit_wait(rt_context* ctx, double timeout_ms, int* pending);

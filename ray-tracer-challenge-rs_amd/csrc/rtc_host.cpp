@@ -1619,11 +1619,19 @@ int rt_debug_normal(rt_context* ctx, uint32_t shape, const double* points, uint6
 
 int rt_context_set_frames_in_flight(rt_context* ctx, uint32_t frames) {
     if (!ctx || frames < 1) return set_error(RT_ERR_INVALID, "bad arguments");
+    // (an A/B setting of RTC_DEBUG wins over the hint)
     std::string v;
-    const bool knob = debug_knob("direct_oversub", &v);  // (an A/B setting wins)
-    if (knob) return RT_OK;
-    ctx->direct_oversub10 = frames > 1 ? 15u : 25u;
-    for (rt_context* p : ctx->peers) p->direct_oversub10 = ctx->direct_oversub10;
+    const bool grid_knob = debug_knob("direct_oversub", &v), split_knob = debug_knob("split", &v);
+    std::vector<rt_context*> ms{ctx};
+    ms.insert(ms.end(), ctx->peers.begin(), ctx->peers.end());
+    for (rt_context* m : ms) {
+        if (!grid_knob) m->direct_oversub10 = frames > 1 ? 15u : 25u;
+        // pool kernels: with the next frame filling a launch's tail, tiles
+        // split only above 1.5x the mean workgroup load (a 4K shard of 8 with
+        // two in flight, round 6: cover 0.104 -> 0.094 ms per frame, table
+        // 0.115 -> 0.113; a frame alone keeps 1.0x)
+        if (!split_knob) m->split_factor = frames > 1 ? 1.5 : 1.0;
+    }
     return RT_OK;
 }
 

@@ -27,6 +27,7 @@ others = []
 for _ in range(INFLIGHT if INFLIGHT > 1 else 0):
     c = rtc_amd.Context(0)
     c.set_jit(rtc_amd.RT_JIT_SYNC)
+    c.set_frames_in_flight(INFLIGHT)  # (rtc.h planning hint, as bench.py sets it)
     c.upload(scene)
     others.append(c)
 with rtc_amd.Context(0) as ctx:
