@@ -691,11 +691,15 @@ def measure(args, tiled, world, rank, local, state_before=None):
         # another on one stream (the K-frame bracket above overlaps frames in
         # flight, so bracket / K is the throughput, not a launch's duration;
         # rocprofv3's average duration agrees with this one).
+        # (planned as a frame alone: the hint back to 1 for it, so rocprof of a
+        # one-in-flight run, which the profile set is, times the same launches)
+        ctx.set_frames_in_flight(1)
         lat = timed_launches(step0, [streams[0]], args.steps)
-        for _ in range(burst):
+        for _ in range(burst + 8):
             step0()
         torch.cuda.synchronize()
         kernel_ms = lat() / args.steps
+        ctx.set_frames_in_flight(inflight)
     else:
         kernel_ms = launch_ms
     line = None

@@ -1630,7 +1630,11 @@ int rt_context_set_frames_in_flight(rt_context* ctx, uint32_t frames) {
         // split only above 1.5x the mean workgroup load (a 4K shard of 8 with
         // two in flight, round 6: cover 0.104 -> 0.094 ms per frame, table
         // 0.115 -> 0.113; a frame alone keeps 1.0x)
-        if (!split_knob) m->split_factor = frames > 1 ? 1.5 : 1.0;
+        const double split = frames > 1 ? 1.5 : 1.0;
+        if (!split_knob && m->split_factor != split) {
+            m->split_factor = split;
+            m->order_valid = false;  // the next launches rebuild the tile order with it
+        }
     }
     return RT_OK;
 }
