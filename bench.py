@@ -596,7 +596,16 @@ def measure(args, tiled, world, rank, local, state_before=None):
         # per-shard render, gather + de-interleave and end-to-end device ms of
         # one frame (rt_render's events; median of 5), every rank collective
         host = np.empty((cam.height, cam.width, 3), dtype=image.cpu().numpy().dtype) if rank == 0 else None
-        sts = [ctx.render_stats(cam, args.depth, args.precision, args.out, host) for _ in range(5)]
+
+        def lone_stats():  # one synchronous frame at a time: planned for one in flight (median of 5)
+            if inflight > 1:
+                ctx.set_frames_in_flight(1)
+            try:
+                return [ctx.render_stats(cam, args.depth, args.precision, args.out, host) for _ in range(5)]
+            finally:
+                if inflight > 1:
+                    ctx.set_frames_in_flight(inflight)
+        sts = lone_stats()
         kernel_ms = float(np.median([st["kernel_ms"] for st in sts]))
         extra = {"render_ms_per_shard": kernel_ms,
                  "gather_ms": float(np.median([st["gather_ms"] for st in sts])),
@@ -616,7 +625,7 @@ def measure(args, tiled, world, rank, local, state_before=None):
         t = time.perf_counter()
         timed()
         el2, _ = rdist.job_totals(time.perf_counter() - t, rays, "cpu")
-        sts2 = [ctx.render_stats(cam, args.depth, args.precision, args.out, host) for _ in range(5)]
+        sts2 = lone_stats()
         variants[other] = {"ms_per_step": el2 * 1e3 / args.steps,
                            "frame_ms": float(np.median([st["frame_ms"] for st in sts2])),
                            "gather_ms": float(np.median([st["gather_ms"] for st in sts2])),
@@ -665,6 +674,10 @@ def measure(args, tiled, world, rank, local, state_before=None):
                 # the 8-way split on this one GPU: each shard's kernel ms (what
                 # rank r renders at N = 8; warm, cost-ordered, median of 3), so
                 # every line carries the slowest of 8 beside its own split
+                # (each launch alone: planned for one frame in flight, as
+                # frame_latency_ms is; the hint for two raises the split
+                # threshold, which lengthens a lone shard: DESIGN.md §6)
+                one.set_frames_in_flight(1)
                 rows8 = rtc_amd.shard_rows(cam.height, 8)
                 strip8 = torch.empty((rows8, cam.width, 3), dtype=rdtype, device="cuda")
                 per8 = []
