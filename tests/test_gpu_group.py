@@ -105,3 +105,33 @@ def test_group_back_to_back_frames(gpu_ctx, group_ctx, rtc):
     for (c, f), o, r in zip(jobs, outs, refs):
         assert np.array_equal(o.cpu().numpy(), r), (c.width, c.height, f)
     assert np.array_equal(host, refs[3])
+
+
+@pytest.mark.parametrize("gather", ["rccl", "peer"])
+def test_two_group_contexts_in_flight(gpu_ctx, rtc, gather):
+    """bench.py's tiled lines with frames in flight: two rank-form groups, each
+    with its own communicator, stream and u8 canvas, rendering alternate
+    frames with no host sync in between and the planning hint for two in
+    flight.  Every frame equals the single-GPU context's."""
+    import torch
+    scene = scene_fixture("cover")
+    cam = rtc.camera_resize(scene.camera, 640, 360)
+    gpu_ctx.upload(scene)
+    ref, _ = gpu_ctx.render(cam, 6, precision="f32", out_format="u8")
+    ctxs = [rtc.Context.rank(0, 1, 0, rtc.comm_unique_id()) for _ in range(2)]
+    try:
+        for c in ctxs:
+            c.set_gather(rtc.RT_GATHER_PEER if gather == "peer" else rtc.RT_GATHER_RCCL)
+            c.upload(scene)
+            c.set_frames_in_flight(2)
+        streams = [torch.cuda.Stream() for _ in ctxs]
+        outs = [torch.zeros((cam.height, cam.width, 3), dtype=torch.uint8, device="cuda") for _ in ctxs]
+        for j in range(10):
+            i = j % 2
+            ctxs[i].render_device(cam, outs[i].data_ptr(), streams[i].cuda_stream, 6, "f32", "u8")
+        torch.cuda.synchronize()
+        for i, o in enumerate(outs):
+            assert np.array_equal(o.cpu().numpy(), ref), f"group {i}"
+    finally:
+        for c in ctxs:
+            c.close()
