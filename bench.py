@@ -854,7 +854,5 @@ def measure(args, tiled, world, rank, local, state_before=None):
     return line if rank == 0 else None
 
 
-
-
 if __name__ == "__main__":
     main()
