@@ -88,8 +88,12 @@ int upload(T** dst, const std::vector<T>& v, hipStream_t s) {
 // kernels' wave-level cull (wave_may_hit).  Acceleration only: a shape is
 // skipped for a wave only when no lane's ray can meet this sphere at t >= 0,
 // so it is padded well beyond the f32/f64 rounding of the local-space tests.
-// Returns radius -1 for unbounded shapes (planes, open-ended cylinders and
-// cones) and for transforms whose forward matrix is not finite.
+// Returns radius -1 for unbounded shapes (planes, open-ended cylinders,
+// every cone) and for transforms whose forward matrix is not finite.
+// Cones: a ray parallel to the side (|a| < EPSILON, |b| > EPSILON) gets the
+// single root -c / 2b with no y-range test (cone.rs:97-99), anywhere on the
+// infinite double cone, so no ball around the finite cone bounds a cone's
+// entries (a random world's grazing ray found it: tests/test_gpu_random_worlds.py).
 void bounding_sphere(const rt_shape_desc& d, double out[4]) {
     out[0] = out[1] = out[2] = 0.0;
     out[3] = -1.0;
@@ -98,12 +102,11 @@ void bounding_sphere(const rt_shape_desc& d, double out[4]) {
     switch (d.kind) {
         case RT_SHAPE_SPHERE: r = 1.0; break;
         case RT_SHAPE_CUBE: r = std::sqrt(3.0); break;
-        case RT_SHAPE_CYLINDER:
-        case RT_SHAPE_CONE: {
+        case RT_SHAPE_CYLINDER: {
             if (!std::isfinite(lo) || !std::isfinite(hi) || !(lo <= hi)) return;
-            const double half = 0.5 * (hi - lo), rad2 = d.kind == RT_SHAPE_CYLINDER ? 1.0 : std::max(lo * lo, hi * hi);
+            const double half = 0.5 * (hi - lo);
             c[1] = 0.5 * (lo + hi);
-            r = std::sqrt(rad2 + half * half);
+            r = std::sqrt(1.0 + half * half);
             break;
         }
         case RT_SHAPE_TRIANGLE: {
@@ -119,7 +122,7 @@ void bounding_sphere(const rt_shape_desc& d, double out[4]) {
                                           (v[2] - c[2]) * (v[2] - c[2])));
             break;
         }
-        default: return;  // plane
+        default: return;  // plane, cone
     }
     hm::M4 inv;
     for (int i = 0; i < 4; ++i)
