@@ -277,7 +277,11 @@ int rt_render_device(rt_context* ctx, const rt_camera_desc* camera,
                      void* hip_stream);
 
 /* Batch World::color_at (world.rs:89-95): rays[i] = {ox,oy,oz,dx,dy,dz},
- * out[i] = RGB, both f64 host arrays; `max_depth` = remaining. */
+ * out[i] = RGB, both f64 host arrays; `max_depth` = remaining.  In a world
+ * with reflective or transparent materials (max_depth > 0) every direction
+ * must be unit length within 1e-6, as the camera's are (camera.rs:66), or
+ * RT_ERR_INVALID: the ray trees' fixed-point pixel sums are bounded for unit
+ * directions, and with eye = -d the specular term grows as |d|^shininess. */
 int rt_color_at(rt_context* ctx, const double* rays, uint64_t n_rays,
                 uint32_t max_depth, uint32_t precision, double* out_rgb,
                 rt_stats* stats);

@@ -1544,6 +1544,22 @@ int rt_color_at(rt_context* ctx, const double* rays, uint64_t n, uint32_t depth,
         if (stats) std::memset(stats, 0, sizeof(*stats));
         return RT_OK;
     }
+    // Worlds with secondary rays run the pool kernel, whose fixed-point pixel
+    // sums are sized for unit directions (check_pixel_range): with |d| != 1
+    // the specular term grows as |d|^shininess (material.rs:100-109, eye =
+    // -d) past any fixed range.  The camera's rays are unit (camera.rs:66),
+    // so only a caller's own rays can be refused here.
+    if ((ctx->w32.scene.any_secondary || ctx->w64.scene.any_secondary) && depth > 0) {
+        for (uint64_t i = 0; i < n; ++i) {
+            const double* d = rays + 6 * i + 3;
+            const double dd = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+            if (!(std::fabs(dd - 1.0) <= 1e-6))
+                return set_error(RT_ERR_INVALID, "rt_color_at: ray " + std::to_string(i) + " has |d|^2 = " +
+                                                     std::to_string(dd) +
+                                                     "; in a world with reflective or transparent materials "
+                                                     "directions must be unit length (within 1e-6)");
+        }
+    }
     RT_HIP(hipSetDevice(ctx->device));
     const size_t elem = precision == RT_PRECISION_F32 ? 4 : 8;
     const size_t in_bytes = n * 6 * sizeof(double), out_bytes = n * 3 * elem;

@@ -26,12 +26,25 @@ F32_PIX_FRAC = 0.99  # observed minimum over the 48 seeds: 0.9958 (round 6)
 SEEDS = list(range(48))
 
 
+def rtc_amd_error():
+    import rtc_amd
+    return rtc_amd.RenderError
+
+
+def depth_has_pool(tables):
+    """Some material reflective or transparent (the pool kernel's worlds)."""
+    return any(m.reflectiveness != 0 or m.transparency != 0 for m in tables.materials)
+
+
 def _counts(st):
     return {k: st[k] for k in ("primary", "shadow", "reflect", "refract", "shaded", "lit_patterned",
                                "refract_evals", "schlick_evals")}
 
 
-def _random_world(seed):
+def _random_world(seed, plain=False, allow_dup=True):
+    """(tables, camera, depth) of seed's world.  plain: no reflective or
+    transparent material (the direct kernel's worlds); allow_dup=False: no
+    value-identical copy.  Neither changes the draws of the other parts."""
     from rtc_amd import world as W
     rng = np.random.default_rng(seed)
 
@@ -100,7 +113,12 @@ def _random_world(seed):
             shapes.append(W.triangle(*pts, material()))
     if rng.random() < 0.25:  # a value-identical copy (the containers walk's identity classes)
         import copy
-        shapes.insert(int(rng.integers(0, len(shapes))), copy.deepcopy(shapes[int(rng.integers(1, len(shapes)))]))
+        at, src = int(rng.integers(0, len(shapes))), int(rng.integers(1, len(shapes)))
+        if allow_dup:
+            shapes.insert(at, copy.deepcopy(shapes[src]))
+    if plain:
+        for sh in shapes:
+            sh.material.reflectiveness = sh.material.transparency = 0.0
     lights = [W.Light((u(-8, 8), u(4, 10), u(-10, -2)), (u(0.3, 1), u(0.3, 1), u(0.3, 1)))
               for _ in range(int(rng.integers(1, 4)))]
     eye = (u(-4, 4), u(1.5, 4), u(-9, -6))
@@ -122,3 +140,52 @@ def test_random_world_parity(gpu_ctx, oracle, seed):
     agree = float((d <= 2).mean())
     print(f"seed {seed} depth {depth} shapes {len(tables.shapes)}: f64 {err:.2e}, f32 within 2/255 {agree:.4f}")
     assert agree >= F32_PIX_FRAC, f"seed {seed}: f32 {agree:.4f}"
+
+
+@pytest.mark.parametrize("plain", [False, True], ids=["pool", "direct"])
+@pytest.mark.parametrize("seed", list(range(8)))
+def test_random_world_per_scene_kernel_equals_generic(rtc, seed, plain):
+    """The per-scene (hipRTC) kernels the bench runs, built for each random
+    world (constant shape records, clusters, world-space spheres and cubes,
+    the acceleration skips), against the generic f32 kernel: the same
+    frame bit for bit and the same counters."""
+    tables, cam, depth = _random_world(seed, plain=plain, allow_dup=False)
+    with rtc.Context(0) as gen, rtc.Context(0) as jit:
+        gen.set_jit(rtc.RT_JIT_OFF)
+        jit.set_jit(rtc.RT_JIT_SYNC)
+        gen.upload(tables)
+        jit.upload(tables)
+        a, sa = gen.render(cam, depth, precision="f32")
+        b, sb = jit.render(cam, depth, precision="f32")
+        assert jit.jit_status()["used"], f"seed {seed}: no per-scene kernel ({jit.jit_status()})"
+        assert np.array_equal(a, b), f"seed {seed}: {int((a != b).any(axis=2).sum())} pixels differ"
+        assert _counts(sa) == _counts(sb)
+
+
+@pytest.mark.parametrize("seed", list(range(16)))
+def test_random_world_color_at_random_rays(gpu_ctx, oracle, seed):
+    """World::color_at (world.rs:89-93) on 2048 random rays per random world:
+    origins anywhere in the scene's box, inside shapes included (the
+    containers walk then starts with entries at t < 0), unit directions.
+    f64 within 1e-9 of the oracle's color_at, counters equal.  (Non-unit
+    directions are refused in worlds with secondary rays, rtc.h rt_color_at:
+    the specular term grows as |d|^shininess past the pool's fixed-point
+    range.)"""
+    tables, _, _ = _random_world(seed)
+    rng = np.random.default_rng(1000 + seed)
+    n = 2048
+    o = rng.uniform([-4, -1.5, -6], [4, 4, 4], size=(n, 3))
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([o, d], axis=1)
+    gpu_ctx.upload(tables)
+    if depth_has_pool(tables):
+        bad = rays.copy()
+        bad[7, 3:] *= 1.5
+        with pytest.raises(rtc_amd_error(), match="unit length"):
+            gpu_ctx.color_at(bad, 6, precision="f64")
+    got, st = gpu_ctx.color_at(rays, 6, precision="f64")
+    ref, rst = oracle.color_at(tables, rays, 6)
+    err = float(np.abs(got - ref).max())
+    assert err < ABS64, f"seed {seed}: max |err| {err:.3g} at ray {int(np.abs(got - ref).max(axis=1).argmax())}"
+    assert _counts(st) == _counts(rst), f"seed {seed}"
