@@ -143,7 +143,7 @@ def test_random_world_parity(gpu_ctx, oracle, seed):
 
 
 @pytest.mark.parametrize("plain", [False, True], ids=["pool", "direct"])
-@pytest.mark.parametrize("seed", list(range(8)))
+@pytest.mark.parametrize("seed", list(range(16)))
 def test_random_world_per_scene_kernel_equals_generic(rtc, seed, plain):
     """The per-scene (hipRTC) kernels the bench runs, built for each random
     world (constant shape records, clusters, world-space spheres and cubes,
