@@ -192,3 +192,59 @@ def test_random_world_color_at_random_rays(gpu_ctx, oracle, seed):
     err = float(np.abs(got - ref).max())
     assert err < ABS64, f"seed {seed}: max |err| {err:.3g} at ray {int(np.abs(got - ref).max(axis=1).argmax())}"
     assert _counts(st) == _counts(rst), f"seed {seed}"
+
+
+def _many_shapes_world(seed, n):
+    """A world of n small shapes (spheres, cubes, closed cylinders, triangles)
+    scattered over a floor, a fifth of them reflective or glass: past the
+    per-scene builds' record limit (255 shapes) and the LDS world tables."""
+    from rtc_amd import world as W
+    rng = np.random.default_rng(seed)
+
+    def u(lo, hi):
+        return float(rng.uniform(lo, hi))
+
+    shapes = [W.plane(W.Material(color=(0.8, 0.8, 0.7), reflectiveness=0.1), W.translation(0, -0.2, 0))]
+    for _ in range(n):
+        m = W.Material(color=(u(0, 1), u(0, 1), u(0, 1)), specular=u(0, 1), shininess=u(10, 200))
+        r = rng.random()
+        if r < 0.1:
+            m.reflectiveness = u(0.2, 0.9)
+        elif r < 0.2:
+            m.transparency, m.refractive_index = u(0.5, 1.0), u(1.1, 1.8)
+        s = u(0.05, 0.25)
+        t = W.mat_mul(W.translation(u(-6, 6), u(0, 3), u(-4, 8)), W.rotation_y(u(0, 3)))
+        k = int(rng.integers(0, 4))
+        if k == 0:
+            shapes.append(W.sphere(m, W.mat_mul(t, W.scaling(s, s, s))))
+        elif k == 1:
+            shapes.append(W.cube(m, W.mat_mul(t, W.scaling(s, s, s))))
+        elif k == 2:
+            shapes.append(W.cylinder(-1, 1, True, m, W.mat_mul(t, W.scaling(s, s, s))))
+        else:
+            c = (u(-6, 6), u(0, 3), u(-4, 8))
+            shapes.append(W.triangle(*[tuple(c[q] + u(-0.3, 0.3) for q in range(3)) for _ in range(3)], m))
+    lights = [W.Light((-10, 10, -10)), W.Light((8, 12, -4), (0.4, 0.4, 0.5))]
+    cam = W.camera(80, 60, 1.1, (0, 2.5, -9), (0, 1, 2), (0, 1, 0))
+    return W.World(lights, shapes).tables(), cam
+
+
+@pytest.mark.parametrize("n", [300, 1500])
+def test_many_shapes_world(gpu_ctx, oracle, rtc, n):
+    """Hundreds to thousands of shapes: f64 within 1e-9 of the oracle with
+    equal counters, f32 within 2/255, and the per-scene kernels (clusters,
+    or the generic tables past 255 shapes) bit-equal to the generic one."""
+    tables, cam = _many_shapes_world(n, n)
+    gpu_ctx.upload(tables)
+    ref, rst = oracle.render(tables, cam, 4, threads=8)
+    img, st = gpu_ctx.render(cam, 4, precision="f64")
+    assert float(np.abs(img - ref).max()) < ABS64
+    assert _counts(st) == _counts(rst)
+    img32, s32 = gpu_ctx.render(cam, 4, precision="f32")
+    d = np.abs(oracle.quantize(img32).astype(int) - oracle.quantize(ref).astype(int)).max(axis=2)
+    assert float((d <= 2).mean()) >= F32_PIX_FRAC
+    with rtc.Context(0) as jit:
+        jit.set_jit(rtc.RT_JIT_SYNC)
+        jit.upload(tables)
+        b, sb = jit.render(cam, 4, precision="f32")
+        assert np.array_equal(img32, b) and _counts(s32) == _counts(sb), jit.jit_status()
