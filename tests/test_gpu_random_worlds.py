@@ -41,10 +41,12 @@ def _counts(st):
                                "refract_evals", "schlick_evals")}
 
 
-def _random_world(seed, plain=False, allow_dup=True):
+def _random_world(seed, plain=False, allow_dup=True, light_scale=1.0):
     """(tables, camera, depth) of seed's world.  plain: no reflective or
     transparent material (the direct kernel's worlds); allow_dup=False: no
-    value-identical copy.  Neither changes the draws of the other parts."""
+    value-identical copy; light_scale: brighter lights (the f32 pixel sums'
+    fixed-point scale follows the world's brightness bound).  None of them
+    changes the draws of the other parts."""
     from rtc_amd import world as W
     rng = np.random.default_rng(seed)
 
@@ -119,16 +121,21 @@ def _random_world(seed, plain=False, allow_dup=True):
     if plain:
         for sh in shapes:
             sh.material.reflectiveness = sh.material.transparency = 0.0
-    lights = [W.Light((u(-8, 8), u(4, 10), u(-10, -2)), (u(0.3, 1), u(0.3, 1), u(0.3, 1)))
+    lights = [W.Light((u(-8, 8), u(4, 10), u(-10, -2)),
+                      (light_scale * u(0.3, 1), light_scale * u(0.3, 1), light_scale * u(0.3, 1)))
               for _ in range(int(rng.integers(1, 4)))]
     eye = (u(-4, 4), u(1.5, 4), u(-9, -6))
     cam = W.camera(96, 72, u(0.6, 1.2), eye, (0, 0.5, 0), (0, 1, 0))
     return W.World(lights, shapes).tables(), cam, int(rng.integers(0, 7))
 
 
-@pytest.mark.parametrize("seed", SEEDS)
+@pytest.mark.parametrize("seed", SEEDS + [f"{s}x4" for s in range(8)])
 def test_random_world_parity(gpu_ctx, oracle, seed):
-    tables, cam, depth = _random_world(seed)
+    """Seeds "<s>x4": the same world with lights four times as bright."""
+    if isinstance(seed, str):
+        tables, cam, depth = _random_world(int(seed[:-2]), light_scale=4.0)
+    else:
+        tables, cam, depth = _random_world(seed)
     gpu_ctx.upload(tables)
     ref, rst = oracle.render(tables, cam, depth, threads=8)
     img, st = gpu_ctx.render(cam, depth, precision="f64")
