@@ -145,6 +145,10 @@ def test_random_world_parity(gpu_ctx, oracle, seed):
     img32, _ = gpu_ctx.render(cam, depth, precision="f32")
     d = np.abs(oracle.quantize(img32).astype(int) - oracle.quantize(ref).astype(int)).max(axis=2)
     agree = float((d <= 2).mean())
+    # the next frames are cost-ordered (heavy tiles split, raised priority): the same pixels
+    for precision, first in (("f32", img32), ("f64", img)):
+        again, _ = gpu_ctx.render(cam, depth, precision=precision)
+        assert np.array_equal(again, first), f"seed {seed}: warm {precision} frame differs"
     print(f"seed {seed} depth {depth} shapes {len(tables.shapes)}: f64 {err:.2e}, f32 within 2/255 {agree:.4f}")
     assert agree >= F32_PIX_FRAC, f"seed {seed}: f32 {agree:.4f}"
 
