@@ -259,3 +259,24 @@ def test_many_shapes_world(gpu_ctx, oracle, rtc, n):
         jit.upload(tables)
         b, sb = jit.render(cam, 4, precision="f32")
         assert np.array_equal(img32, b) and _counts(s32) == _counts(sb), jit.jit_status()
+
+
+@pytest.mark.parametrize("seed", list(range(24)))
+def test_random_world_accelerations_are_exact(gpu_ctx, rtc, monkeypatch, seed):
+    """The wave cull and the shadow/exit skips are acceleration only: on every
+    random world the f32 and f64 frames with the cull off (RTC_DEBUG=cull=0,
+    every shape unbounded) and with RT_FLAG_NO_SKIPS equal the default frame
+    bit for bit, counters included.  (An f32 decision flipped on one pixel
+    would pass the oracle's 2/255 floor; this catches it.)"""
+    tables, cam, depth = _random_world(seed)
+    gpu_ctx.upload(tables)
+    monkeypatch.setenv("RTC_DEBUG", "cull=0")
+    with rtc.Context(0) as nocull:
+        nocull.upload(tables)
+        for precision in ("f32", "f64"):
+            a, sa = gpu_ctx.render(cam, depth, precision=precision)
+            b, sb = nocull.render(cam, depth, precision=precision)
+            c, sc = gpu_ctx.render(cam, depth, precision=precision, flags=rtc.RT_FLAG_NO_SKIPS)
+            assert np.array_equal(a, b), f"seed {seed} {precision}: the cull changed {int((a != b).any(axis=2).sum())} px"
+            assert np.array_equal(a, c), f"seed {seed} {precision}: the skips changed {int((a != c).any(axis=2).sum())} px"
+            assert _counts(sa) == _counts(sb) == _counts(sc)
