@@ -513,7 +513,8 @@ class Context:
                                      C.c_void_p(stream_ptr or 0)))
 
     def color_at(self, rays, depth: int = RT_DEFAULT_MAX_DEPTH, precision: str = "f32"):
-        """Batched World::color_at: rays (n, 6) = origin, direction -> colours (n, 3) f64."""
+        """Batched World::color_at: rays (n, 6) = origin, direction -> colours (n, 3) f64.  In a world with
+        reflective or transparent materials the directions must be unit length (rtc.h rt_color_at)."""
         r = np.ascontiguousarray(np.asarray(rays, dtype=np.float64).reshape(-1, 6))
         out = np.zeros((r.shape[0], 3), dtype=np.float64)
         st = Stats()
