@@ -561,8 +561,23 @@ def measure(args, tiled, world, rank, local, state_before=None):
     # stream (per-launch event records cost ~6 us of GPU time per 1080p frame
     # on MI355X — they stop the next launch's waves from overlapping the
     # previous one's tail — see scripts/host_overhead.py): average = bracket / K.
-    # Tiled: the bracket is rank 0's stream (its shard, the gather, the de-interleave).
-    timed = timed_launches(step, streams, args.steps)
+    # Only a line of one frame at a time uses the bracket (its roofline launch
+    # duration).  With frames in flight the bracket needs cross-stream joins at
+    # both ends, which cost ~0.8 us per frame of a 20-frame region
+    # (scripts/region_inflight_probe.py), and its average is a throughput, not
+    # a launch's duration: the region is then the K frames and the
+    # synchronize alone, and the roofline takes frame_latency_ms (below).
+    # Tiled lines take their launch duration from rt_render's events.
+    use_events = not tiled and inflight == 1
+    bracket = timed_launches(step, streams, args.steps) if use_events else None
+
+    def timed():
+        if bracket is not None:
+            return bracket()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        return None
     # The GPU should not sit idle between the warm-up and the timed region
     # (the events and the barrier above cost milliseconds): ~2 ms of untimed
     # frames keep it busy across them; the region itself is unchanged.
@@ -575,7 +590,7 @@ def measure(args, tiled, world, rank, local, state_before=None):
     turn[0] = 0
     before = counters_sum()  # (a few-us copy per context: the region's rays are after - before)
     t0 = time.perf_counter()
-    launch_ms = timed() / args.steps  # ends with torch.cuda.synchronize()
+    bracket_ms = timed()  # ends with torch.cuda.synchronize()
     # each rank's clock stops at its own synchronize; the closing barrier is
     # outside it (a gloo barrier costs ~0.1-1 ms against a 7 ms 20-frame tiled
     # region) and the max over ranks is taken below (rdist.job_totals).  In
@@ -714,7 +729,7 @@ def measure(args, tiled, world, rank, local, state_before=None):
         kernel_ms = lat() / args.steps
         ctx.set_frames_in_flight(inflight)
     else:
-        kernel_ms = launch_ms
+        kernel_ms = bracket_ms / args.steps
     line = None
     if rank == 0:
         flops_per_launch = flops / args.steps
