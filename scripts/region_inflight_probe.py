@@ -9,7 +9,8 @@ synchronizes:
             cross-stream wait, K frames, joins + event, sync (bench.py)
   nocount   bench without the counters read before t0
   nojoin    t0, K frames, sync (no events, no cross-stream waits)
-Median and min us per frame over ROUNDS rounds, plus the 1000-frame rate.
+Median and min us per frame over ROUNDS rounds, plus the 1000-frame rate and
+the host's own submission time per frame within it.
 Usage (GPU box): python scripts/region_inflight_probe.py [rounds]"""
 import json
 import os
@@ -83,10 +84,13 @@ def main():
     t0 = time.perf_counter()
     for _ in range(1000):
         step()
+    t1 = time.perf_counter()
     torch.cuda.synchronize()
     steady = (time.perf_counter() - t0) * 1e6 / 1000
+    host_submit = (t1 - t0) * 1e6 / 1000  # the host's own time per step (no wait on the GPU)
     out = {v: {"median_us": round(statistics.median(x), 2), "min_us": round(min(x), 2)} for v, x in res.items()}
     out["steady_1000_us"] = round(steady, 2)
+    out["host_submit_us"] = round(host_submit, 2)
     print(json.dumps(out), flush=True)
     for c in ctxs:
         c.close()
