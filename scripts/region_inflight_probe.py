@@ -9,6 +9,7 @@ synchronizes:
             cross-stream wait, K frames, joins + event, sync (bench.py)
   nocount   bench without the counters read before t0
   nojoin    t0, K frames, sync (no events, no cross-stream waits)
+  spin      nojoin with the host polling each stream's last event before the sync
 Median and min us per frame over ROUNDS rounds, plus the 1000-frame rate and
 the host's own submission time per frame within it.
 Usage (GPU box): python scripts/region_inflight_probe.py [rounds]"""
@@ -72,11 +73,22 @@ def main():
             for _ in range(k):
                 step()
             torch.cuda.synchronize()
+        elif variant == "spin":  # nojoin, but the host polls the streams' last events before synchronizing
+            for _ in range(k):
+                step()
+            for e, st in zip(ends, streams):
+                e.record(st)
+            while not all(e.query() for e in ends):
+                pass
+            torch.cuda.synchronize()
         else:
             timed()
         return (time.perf_counter() - t0) * 1e6 / k
 
-    res = {v: [] for v in ("bench", "nocount", "nojoin")}
+    ends = [torch.cuda.Event() for _ in streams]
+    for e, st in zip(ends, streams):
+        e.record(st)
+    res = {v: [] for v in ("bench", "nocount", "nojoin", "spin")}
     for _ in range(rounds):
         for v in res:
             res[v].append(region(v))
