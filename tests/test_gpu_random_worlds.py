@@ -159,7 +159,8 @@ def test_random_world_per_scene_kernel_equals_generic(rtc, seed, plain):
     """The per-scene (hipRTC) kernels the bench runs, built for each random
     world (constant shape records, clusters, world-space spheres and cubes,
     the acceleration skips), against the generic f32 kernel: the same
-    frame bit for bit and the same counters."""
+    frame bit for bit and the same counters.  (21 of these 32 builds were
+    accepted in round 6; the others were refused for scratch.)"""
     tables, cam, depth = _random_world(seed, plain=plain, allow_dup=False)
     with rtc.Context(0) as gen, rtc.Context(0) as jit:
         gen.set_jit(rtc.RT_JIT_OFF)
@@ -169,9 +170,11 @@ def test_random_world_per_scene_kernel_equals_generic(rtc, seed, plain):
         a, sa = gen.render(cam, depth, precision="f32")
         b, sb = jit.render(cam, depth, precision="f32")
         js = jit.jit_status()
-        if not js["used"]:  # a build that spills or loses occupancy is refused (rtc_jit.cpp jit_variant)
-            assert "not used" in js["log"], js
-            pytest.skip(f"seed {seed}: {js['log']}")
+        if not js["used"]:
+            # a build that spills or loses occupancy is refused (rtc_jit.cpp
+            # jit_variant), with its reason in the log, and the frame falls
+            # back to the generic kernel (checked below like an accepted one)
+            assert "not used" in js["log"] and ("scratch" in js["log"] or "workgroups/CU" in js["log"]), js
         assert np.array_equal(a, b), f"seed {seed}: {int((a != b).any(axis=2).sum())} pixels differ"
         assert _counts(sa) == _counts(sb)
 
