@@ -81,10 +81,11 @@ def parse():
                          "measured too and reported under gather_variants")
     ap.add_argument("--ab", action="store_true",
                     help="A/B runs: skip the one-shot child, the host-frame latency and the per-generation frame")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight: consecutive steps alternate between this many contexts, each on a "
                          "stream of its own, so one frame's launch tail overlaps the next frame's start (1 = "
-                         "every frame on one stream, one after another)")
+                         "every frame on one stream, one after another); default 3 for frames, 2 when tiled "
+                         "(each a group context with its own RCCL communicator)")
     ap.add_argument("--stream", choices=["side", "null"], default="side",
                     help="the launch stream: a stream of the bench's own (default) or HIP's null stream")
     ap.add_argument("--one-shot-child", action="store_true", help=argparse.SUPPRESS)
@@ -449,7 +450,11 @@ def measure(args, tiled, world, rank, local, state_before=None):
     # table's 0.141 -> 0.114, reflect_refract 0.236 -> 0.220; frames equal.
     # Each frame is whole and independent (a context renders it from its own
     # resident scene copy), as a renderer producing an animation would run.
-    inflight = max(1, args.inflight)
+    # Default 3 for frames: same box, the driver's flags, eight alternating
+    # rounds, 3 ahead of 2 in every one (mean 308.5 against 293.5 Gray/s;
+    # 4: 253-274), equal at 1000 frames (profiles/ab/r06_inflight_3.txt).
+    # Tiled lines keep 2 (equal at N = 1, one communicator per frame in flight).
+    inflight = max(1, args.inflight if args.inflight else (2 if tiled else 3))
     # the frames run on streams of their own (HIP's null stream orders every
     # launch against the device's other blocking streams; --stream null keeps
     # it for the A/B, with one frame in flight)

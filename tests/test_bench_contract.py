@@ -40,8 +40,8 @@ def test_bench_line_contract():
     assert d["unit"] == "Mray/s" and d["dtype"] == "f32" and d["scaling"] == "weak"
     assert d["config"]["rays_per_frame"] == 2 * 320 * 240
     assert d["value"] > 0 and d["ms_per_step"] > 0
-    # frames in flight (two contexts alternating) and one frame's own device time
-    assert d["frames_in_flight"] == 2 and d["frame_latency_ms"] > 0
+    # frames in flight (three contexts alternating) and one frame's own device time
+    assert d["frames_in_flight"] == 3 and d["frame_latency_ms"] > 0
     assert d["frame_latency_ms"] == d["roofline"]["kernel_ms"]
     rl = d["roofline"]
     assert rl["unit"] == "TFLOP/s" and rl["peak"] == 157.3 and 0 < rl["frac"] < 1
